@@ -1,0 +1,61 @@
+# Build for the MI355X path tracer.  Targets:
+#   make            host lib + HIP lib + CLI + oracle (everything __graft_entry__.build() needs)
+#   make hip        cuda_raytracing_amd/lib/librt_hip.so    (hipcc, gfx950)
+#   make host       cuda_raytracing_amd/lib/librt_host.so   (g++)
+#   make oracle     oracle/_build/liboracle_rt.so           (gcc + OpenMP; test infrastructure)
+#   make cli        bin/raytracing                          (reference CLI surface)
+#   make kat        regenerate tests/golden/rng_kat.json from rocRAND
+
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+ARCH      ?= gfx950
+CXX       ?= g++
+CC        ?= gcc
+
+LIBDIR    := cuda_raytracing_amd/lib
+CSRC      := cuda_raytracing_amd/csrc
+INC       := -Iinclude -I$(CSRC)
+
+# No FP contraction anywhere on the path: parity with the oracle is bit-exact.
+HOST_FLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra
+HIP_FLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+              -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-rdc -Wall
+ORACLE_FLAGS := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -fopenmp -Wall -Wextra
+
+HOST_SRC := $(CSRC)/host/rt_host.cpp
+HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp
+HIP_HDR  := $(wildcard $(CSRC)/*.h) include/rt_render.h include/rt_ref_layout.h
+
+all: host hip oracle cli
+
+host: $(LIBDIR)/librt_host.so
+hip: $(LIBDIR)/librt_hip.so
+oracle: oracle/_build/liboracle_rt.so
+cli: bin/raytracing
+
+$(LIBDIR)/librt_host.so: $(HOST_SRC) $(CSRC)/host/glibc_rand.h include/rt_host.h include/rt_ref_layout.h
+	@mkdir -p $(LIBDIR)
+	$(CXX) $(HOST_FLAGS) $(INC) -shared $(HOST_SRC) -o $@
+
+$(LIBDIR)/librt_hip.so: $(HIP_SRC) $(HIP_HDR)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) $(HIP_FLAGS) $(INC) -shared $(HIP_SRC) -o $@
+
+oracle/_build/liboracle_rt.so: oracle/oracle_rt.c include/rt_render.h include/rt_ref_layout.h
+	@mkdir -p oracle/_build
+	$(CC) $(ORACLE_FLAGS) -Iinclude -shared oracle/oracle_rt.c -o $@ -lm
+
+bin/raytracing: $(CSRC)/host/cli.cpp $(LIBDIR)/librt_host.so $(LIBDIR)/librt_hip.so include/rt_host.h
+	@mkdir -p bin
+	$(CXX) $(HOST_FLAGS) $(INC) $(CSRC)/host/cli.cpp -o $@ -L$(LIBDIR) -lrt_host -lrt_hip \
+	  -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
+
+kat:
+	$(CXX) -O1 -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include oracle/kat/gen_rocrand_kat.cpp \
+	  -o oracle/_build/gen_rocrand_kat -L$(ROCM)/lib -lamdhip64 -Wno-deprecated-declarations
+	oracle/_build/gen_rocrand_kat > tests/golden/rng_kat.json
+
+clean:
+	rm -rf $(LIBDIR)/*.so oracle/_build bin
+
+.PHONY: all host hip oracle cli kat clean

@@ -1,0 +1,253 @@
+"""cuda_raytracing_amd — MI355X-native drop-in for luk-zm/cuda_raytracing's per-pixel render path.
+
+Layers:
+  host (librt_host.so, C++)   scene catalog + builder API, BVH, camera, tonemap/PPM
+  device (librt_hip.so, HIP)  rt_render / rt_context_*: RNG seeding + the render kernel on gfx950
+  this module                 thin Python mirror of the reference's surface for tests and bench
+
+The render entry points call the HIP library only; a missing library is an error, never a fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import (Camera, Params, Scene, Settings, Stats, Vec3, vec3, RT_FLAG_COUNT,
+                   RT_FLAG_GLOBAL_SCENE, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
+                   RT_XF_TRANSLATE, RT_XF_YROTATE, RT_XF_YROTATE_TRANSLATE)
+
+__all__ = [
+    "World", "Camera", "Params", "Scene", "Settings", "Stats", "vec3", "build_scene",
+    "camera_from_settings", "make_params", "render", "RenderContext", "tonemap", "write_ppm",
+    "scene_name", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
+    "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError",
+]
+
+
+class RenderError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: {_abi.status_string(code)} ({code})")
+        self.code = code
+
+
+def _check(code: int, what: str) -> None:
+    if code != _abi.RT_OK:
+        raise RenderError(code, what)
+
+
+def scene_name(index: int) -> str:
+    n = _abi.host_lib().rt_scene_name(index)
+    return n.decode() if n else ""
+
+
+class World:
+    """Owns a reference-layout scene (records, refs, texture arena) built on the host.
+
+    Mirrors `World` + the `add_*` builder API of raytracing.cu:1608-1612,1775-1977.  Each World has
+    its own glibc-rand stream seeded with 1, like a fresh reference process.
+    """
+
+    def __init__(self, capacity: int = 8000, arena_bytes: int = 10 << 20):
+        self._L = _abi.host_lib()
+        self._w = self._L.rt_world_create(capacity, arena_bytes)
+        if not self._w:
+            raise MemoryError("rt_world_create failed")
+        self.root: int | None = None
+
+    def __del__(self):
+        w = getattr(self, "_w", None)
+        if w:
+            self._L.rt_world_destroy(w)
+            self._w = None
+
+    # --- catalog (main.cu:52-117) ---
+    def build_scene(self, index: int) -> Settings:
+        s = Settings()
+        _check(self._L.rt_world_build_scene(self._w, index, C.byref(s)), f"build scene {index}")
+        return s
+
+    # --- materials ---
+    def lambert(self, rgb) -> _abi.Material:
+        return self._L.rt_mat_lambert_solid(self._w, vec3(*rgb))
+
+    def light(self, rgb) -> _abi.Material:
+        return self._L.rt_mat_light_solid(self._w, vec3(*rgb))
+
+    def noise(self, scale: float) -> _abi.Material:
+        return self._L.rt_mat_lambert_noise(self._w, scale)
+
+    def checker(self, scale: float, even, odd) -> _abi.Material:
+        return self._L.rt_mat_lambert_checker(self._w, scale, vec3(*even), vec3(*odd))
+
+    def image(self, name: str = "earthmap.jpg") -> _abi.Material:
+        return self._L.rt_mat_lambert_image(self._w, name.encode())
+
+    def metal(self, rgb, fuzz: float) -> _abi.Material:
+        return self._L.rt_mat_metal(vec3(*rgb), fuzz)
+
+    def dielectric(self, ior: float) -> _abi.Material:
+        return self._L.rt_mat_dielectric(ior)
+
+    # --- primitives; xf = RT_XF_* transform ---
+    def sphere(self, center, radius, mat, xf=RT_XF_NONE, angle=0.0, offset=(0, 0, 0)) -> int:
+        return self._L.rt_add_sphere(self._w, xf, angle, vec3(*offset), vec3(*center), radius, mat)
+
+    def moving_sphere(self, center, motion, radius, mat, xf=RT_XF_NONE, angle=0.0, offset=(0, 0, 0)) -> int:
+        return self._L.rt_add_moving_sphere(self._w, xf, angle, vec3(*offset), vec3(*center),
+                                            vec3(*motion), radius, mat)
+
+    def quad(self, q, u, v, mat, xf=RT_XF_NONE, angle=0.0, offset=(0, 0, 0)) -> int:
+        return self._L.rt_add_quad(self._w, xf, angle, vec3(*offset), vec3(*q), vec3(*u), vec3(*v), mat)
+
+    def triangle(self, q, u, v, mat, xf=RT_XF_NONE, angle=0.0, offset=(0, 0, 0)) -> int:
+        return self._L.rt_add_triangle(self._w, xf, angle, vec3(*offset), vec3(*q), vec3(*u), vec3(*v), mat)
+
+    def box(self, a, b, mat, xf=RT_XF_NONE, angle=0.0, offset=(0, 0, 0)) -> int:
+        return self._L.rt_add_box(self._w, xf, angle, vec3(*offset), vec3(*a), vec3(*b), mat)
+
+    def pyramid(self, a, b, tip, mat, xf=RT_XF_NONE, angle=0.0, offset=(0, 0, 0)) -> int:
+        return self._L.rt_add_pyramid(self._w, xf, angle, vec3(*offset), vec3(*a), vec3(*b), vec3(*tip), mat)
+
+    def rand(self) -> int:
+        return self._L.rt_world_rand(self._w)
+
+    # --- BVH + export ---
+    def build_bvh(self) -> int:
+        root = C.c_uint16()
+        _check(self._L.rt_world_build_bvh(self._w, C.byref(root)), "make_bvh")
+        self.root = root.value
+        return self.root
+
+    def scene(self) -> Scene:
+        if self.root is None:
+            self.build_bvh()
+        sc = Scene()
+        _check(self._L.rt_world_scene(self._w, self.root, C.byref(sc)), "scene view")
+        sc._owner = self   # keep the world alive while the view is used
+        return sc
+
+    def blobs(self) -> dict:
+        """Copies of the scene bytes: records, refs, arena (fixtures, tests)."""
+        sc = self.scene()
+        rec = C.string_at(sc.hittables, sc.hittable_count * _abi.HITTABLE_BYTES)
+        refs = np.ctypeslib.as_array(sc.refs, shape=(sc.ref_count,)).copy()
+        tex = C.string_at(sc.textures, sc.texture_bytes) if sc.texture_bytes else b""
+        return {"hittables": rec, "refs": refs, "textures": tex, "root": sc.root}
+
+    def reference_stack_depth(self) -> int:
+        sc = self.scene()
+        d = C.c_uint32()
+        _check(self._L.rt_reference_stack_depth(C.byref(sc), C.byref(d)), "stack depth")
+        return d.value
+
+
+class BlobScene:
+    """A scene held as raw reference-layout bytes (e.g. loaded from tests/golden fixtures)."""
+
+    def __init__(self, hittables: bytes, refs, textures: bytes, root: int):
+        self._rec = C.create_string_buffer(bytes(hittables), len(hittables) or 1)
+        self._refs = np.ascontiguousarray(np.asarray(refs, dtype=np.uint16))
+        self._tex = C.create_string_buffer(bytes(textures), len(textures) or 1)
+        self.count = len(hittables) // _abi.HITTABLE_BYTES
+        self.ntex = len(textures)
+        self.root = int(root)
+
+    def scene(self) -> Scene:
+        sc = Scene()
+        sc.hittables = C.cast(self._rec, C.c_void_p)
+        sc.hittable_count = self.count
+        sc.refs = self._refs.ctypes.data_as(C.POINTER(C.c_uint16))
+        sc.ref_count = len(self._refs)
+        sc.root = self.root
+        sc.textures = C.cast(self._tex, C.POINTER(C.c_uint8))
+        sc.texture_bytes = self.ntex
+        sc._owner = self
+        return sc
+
+
+def build_scene(index: int, capacity: int | None = None):
+    """Catalog scene -> (World, Settings) with the BVH built (the reference's main + make_bvh)."""
+    if capacity is None:
+        capacity = 24000 if index == RT_SCENE_RANDOM_10K else 8000
+    w = World(capacity=capacity)
+    s = w.build_scene(index)
+    w.build_bvh()
+    return w, s
+
+
+def camera_from_settings(settings: Settings, width: int = 0, height: int = 0):
+    """raytracing.cu:1657-1692.  width/height 0 => the reference's W and (int)(W/ratio)."""
+    cam = Camera()
+    W, H = C.c_int32(), C.c_int32()
+    _check(_abi.host_lib().rt_camera_from_settings(C.byref(settings), width, height, C.byref(cam),
+                                                   C.byref(W), C.byref(H)), "camera")
+    return cam, W.value, H.value
+
+
+def make_params(settings: Settings, width: int, height: int, spp: int | None = None,
+                bounces: int | None = None, row_offset: int = 0, row_stride: int = 1,
+                row_count: int | None = None, seed: int = 1234, flags: int = 0) -> Params:
+    p = Params()
+    p.width, p.height = width, height
+    p.row_offset, p.row_stride = row_offset, row_stride
+    p.row_count = row_count if row_count is not None else len(range(row_offset, height, row_stride))
+    p.samples_per_pixel = settings.samples_per_pixel if spp is None else spp
+    p.max_bounces = settings.max_bounces if bounces is None else bounces
+    p.background = settings.background
+    p.seed = seed
+    p.flags = flags
+    return p
+
+
+def render(scene: Scene, camera: Camera, params: Params, with_stats: bool = False):
+    """One-shot GPU render (rt_render): float32 array [row_count, width, 3], linear RGB."""
+    out = np.zeros((params.row_count, params.width, 3), dtype=np.float32)
+    st = Stats()
+    _check(_abi.hip_lib().rt_render(C.byref(scene), C.byref(camera), C.byref(params),
+                                    out.ctypes.data_as(C.c_void_p), C.byref(st)), "rt_render")
+    return (out, st) if with_stats else out
+
+
+class RenderContext:
+    """Device-resident scene (rt_context_*): render into caller device buffers on a HIP stream."""
+
+    def __init__(self, scene: Scene, device: int = 0):
+        self._L = _abi.hip_lib()
+        h = C.c_void_p()
+        _check(self._L.rt_context_create(C.byref(scene), device, C.byref(h)), "rt_context_create")
+        self._h = h
+        self._scene = scene
+
+    def render_into(self, camera: Camera, params: Params, out_device_ptr: int, stream: int = 0) -> None:
+        _check(self._L.rt_context_render(self._h, C.byref(camera), C.byref(params),
+                                         C.c_void_p(out_device_ptr), C.c_void_p(stream)), "rt_context_render")
+
+    def timing(self) -> Stats:
+        st = Stats()
+        _check(self._L.rt_context_timing(self._h, C.byref(st)), "rt_context_timing")
+        return st
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._L.rt_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def tonemap(rgb: np.ndarray) -> np.ndarray:
+    """raytracing.cu:1391-1395,1419-1433: sqrt gamma, clamp [0,0.999], x256 -> u8."""
+    src = np.ascontiguousarray(rgb, dtype=np.float32)
+    out = np.empty(src.shape, dtype=np.uint8)
+    _abi.host_lib().rt_tonemap(src.ctypes.data_as(C.c_void_p), src.size // 3, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def write_ppm(path: str, rgb: np.ndarray) -> None:
+    src = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = src.shape[:2]
+    _check(_abi.host_lib().rt_write_ppm(path.encode(), src.ctypes.data_as(C.c_void_p), w, h), "write_ppm")

@@ -1,0 +1,220 @@
+"""ctypes mirror of include/rt_render.h, include/rt_host.h and include/rt_ref_layout.h.
+
+The C-ABI is the product boundary.  This module only declares the structs
+and loads the shared libraries; it contains no rendering logic.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_DIR = PKG_DIR / "lib"
+HIP_LIB = LIB_DIR / "librt_hip.so"
+HOST_LIB = LIB_DIR / "librt_host.so"
+ORACLE_LIB = REPO_DIR / "oracle" / "_build" / "liboracle_rt.so"
+
+RT_OK = 0
+RT_ERR_INVALID_ARG = -1
+RT_ERR_SCENE = -2
+RT_ERR_HIP = -3
+RT_ERR_NO_DEVICE = -4
+RT_ERR_STACK = -5
+RT_ERR_UNSUPPORTED = -6
+
+RT_FLAG_COUNT = 0x1
+RT_FLAG_GLOBAL_SCENE = 0x2
+
+CNT_NAMES = [
+    "visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate",
+    "visit_yrotate", "visit_group", "bounces", "shades", "perlin", "rng_draws", "samples",
+    "max_stack", "stack_overflow", "reserved14", "reserved15",
+]
+
+RT_XF_NONE, RT_XF_TRANSLATE, RT_XF_YROTATE, RT_XF_YROTATE_TRANSLATE = 0, 1, 2, 3
+RT_SCENE_COUNT = 21
+RT_SCENE_RANDOM_10K = 20
+HITTABLE_BYTES = 120
+TEXTURE_BYTES = 32
+
+
+class Vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+    def tolist(self):
+        return [self.x, self.y, self.z]
+
+
+def vec3(x, y, z) -> Vec3:
+    return Vec3(float(x), float(y), float(z))
+
+
+class Material(C.Structure):
+    """rtr_material: 24 bytes (raytracing.cu:86-99); treated as an opaque value here."""
+    _fields_ = [("kind", C.c_uint32), ("pad_", C.c_uint32), ("payload", C.c_uint8 * 16)]
+
+
+class Scene(C.Structure):
+    _fields_ = [
+        ("hittables", C.c_void_p), ("hittable_count", C.c_uint32),
+        ("refs", C.POINTER(C.c_uint16)), ("ref_count", C.c_uint32),
+        ("root", C.c_uint16), ("pad_", C.c_uint16),
+        ("textures", C.POINTER(C.c_uint8)), ("texture_bytes", C.c_uint64),
+    ]
+
+
+class Camera(C.Structure):
+    _fields_ = [
+        ("pixel00", Vec3), ("delta_u", Vec3), ("delta_v", Vec3), ("center", Vec3),
+        ("defocus_u", Vec3), ("defocus_v", Vec3), ("defocus_angle", C.c_float),
+    ]
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("width", C.c_int32), ("height", C.c_int32),
+        ("row_offset", C.c_int32), ("row_stride", C.c_int32), ("row_count", C.c_int32),
+        ("samples_per_pixel", C.c_int32), ("max_bounces", C.c_int32),
+        ("background", Vec3), ("seed", C.c_uint64), ("flags", C.c_uint32), ("pad_", C.c_uint32),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("init_ms", C.c_double), ("render_ms", C.c_double), ("total_ms", C.c_double),
+        ("samples", C.c_uint64), ("counters", C.c_uint64 * 16),
+        ("stack_needed", C.c_int32), ("scene_in_lds", C.c_int32),
+    ]
+
+    def counter_dict(self):
+        return {n: int(self.counters[i]) for i, n in enumerate(CNT_NAMES) if not n.startswith("reserved")}
+
+
+class Settings(C.Structure):
+    _fields_ = [
+        ("img_ratio", C.c_float), ("img_width", C.c_int32), ("samples_per_pixel", C.c_int32),
+        ("max_bounces", C.c_int32), ("vfov", C.c_float),
+        ("lookfrom", Vec3), ("lookat", Vec3), ("view_up", Vec3),
+        ("defocus_angle", C.c_float), ("background", Vec3), ("img_name", C.c_char * 64),
+    ]
+
+
+def _sig(fn, restype, *argtypes):
+    fn.restype = restype
+    fn.argtypes = list(argtypes)
+    return fn
+
+
+_host = None
+_hip = None
+_oracle = None
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        if not HOST_LIB.exists():
+            raise RuntimeError(f"{HOST_LIB} missing: run `make host` (or __graft_entry__.build())")
+        L = C.CDLL(str(HOST_LIB))
+        P = C.c_void_p
+        _sig(L.rt_world_create, P, C.c_uint32, C.c_uint64)
+        _sig(L.rt_world_destroy, None, P)
+        _sig(L.rt_settings_default, None, C.POINTER(Settings))
+        _sig(L.rt_world_build_scene, C.c_int, P, C.c_int, C.POINTER(Settings))
+        _sig(L.rt_world_build_bvh, C.c_int, P, C.POINTER(C.c_uint16))
+        _sig(L.rt_world_scene, C.c_int, P, C.c_uint16, C.POINTER(Scene))
+        _sig(L.rt_world_hittable_count, C.c_uint32, P)
+        _sig(L.rt_world_ref_count, C.c_uint32, P)
+        _sig(L.rt_world_texture_bytes, C.c_uint64, P)
+        _sig(L.rt_world_rand, C.c_int32, P)
+        _sig(L.rt_scene_name, C.c_char_p, C.c_int)
+        for name in ("rt_mat_lambert_solid", "rt_mat_light_solid"):
+            _sig(getattr(L, name), Material, P, Vec3)
+        _sig(L.rt_mat_lambert_image, Material, P, C.c_char_p)
+        _sig(L.rt_mat_lambert_noise, Material, P, C.c_float)
+        _sig(L.rt_mat_metal, Material, Vec3, C.c_float)
+        _sig(L.rt_mat_dielectric, Material, C.c_float)
+        _sig(L.rt_mat_lambert_checker, Material, P, C.c_float, Vec3, Vec3)
+        xf = (P, C.c_int, C.c_float, Vec3)
+        _sig(L.rt_add_sphere, C.c_int, *xf, Vec3, C.c_float, Material)
+        _sig(L.rt_add_moving_sphere, C.c_int, *xf, Vec3, Vec3, C.c_float, Material)
+        _sig(L.rt_add_quad, C.c_int, *xf, Vec3, Vec3, Vec3, Material)
+        _sig(L.rt_add_triangle, C.c_int, *xf, Vec3, Vec3, Vec3, Material)
+        _sig(L.rt_add_box, C.c_int, *xf, Vec3, Vec3, Material)
+        _sig(L.rt_add_pyramid, C.c_int, *xf, Vec3, Vec3, Vec3, Material)
+        _sig(L.rt_camera_from_settings, C.c_int, C.POINTER(Settings), C.c_int32, C.c_int32,
+             C.POINTER(Camera), C.POINTER(C.c_int32), C.POINTER(C.c_int32))
+        _sig(L.rt_reference_stack_depth, C.c_int, C.POINTER(Scene), C.POINTER(C.c_uint32))
+        _sig(L.rt_tonemap, None, C.c_void_p, C.c_size_t, C.c_void_p)
+        _sig(L.rt_write_ppm, C.c_int, C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32)
+        _host = L
+    return _host
+
+
+HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_timing",
+               "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version"]
+
+
+def _bind_single_hip_runtime():
+    """Keep ONE HIP runtime per process.
+
+    PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7, the same as /opt/rocm's).  If
+    torch's copy is loaded first, librt_hip.so's DT_NEEDED resolves to it by SONAME and the process has
+    one runtime.  If ours were loaded first, torch would later map a second runtime and see no GPUs.
+    So when torch is installed we import it before dlopen-ing the render library.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
+def hip_lib():
+    """The MI355X render library.  Raises (never falls back) when it is missing."""
+    global _hip
+    if _hip is None:
+        if not HIP_LIB.exists():
+            raise RuntimeError(f"{HIP_LIB} missing: the HIP render path is not built "
+                               "(run `make hip` / __graft_entry__.build()); there is no CPU fallback")
+        _bind_single_hip_runtime()
+        L = C.CDLL(str(HIP_LIB))
+        P = C.c_void_p
+        _sig(L.rt_render, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), P,
+             C.POINTER(Stats))
+        _sig(L.rt_context_create, C.c_int, C.POINTER(Scene), C.c_int, C.POINTER(C.c_void_p))
+        _sig(L.rt_context_render, C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P)
+        _sig(L.rt_context_timing, C.c_int, P, C.POINTER(Stats))
+        _sig(L.rt_context_destroy, None, P)
+        _sig(L.rt_status_string, C.c_char_p, C.c_int)
+        _sig(L.rt_device_count, C.c_int, C.POINTER(C.c_int))
+        _sig(L.rt_abi_version, C.c_int)
+        _hip = L
+    return _hip
+
+
+def oracle_lib():
+    """CPU oracle — test infrastructure only (tests/, smoke(), bench.py cpu_baseline)."""
+    global _oracle
+    if _oracle is None:
+        if not ORACLE_LIB.exists():
+            raise RuntimeError(f"{ORACLE_LIB} missing: run `make oracle`")
+        L = C.CDLL(str(ORACLE_LIB))
+        _sig(L.rt_render_cpu, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
+             C.c_void_p, C.POINTER(Stats))
+        _sig(L.rt_oracle_sinf, C.c_float, C.c_float)
+        _sig(L.rt_oracle_pow5f, C.c_float, C.c_float)
+        _sig(L.rt_oracle_uniforms, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int)
+        _oracle = L
+    return _oracle
+
+
+def status_string(code: int) -> str:
+    names = {0: "ok", -1: "invalid argument", -2: "malformed scene", -3: "HIP runtime error",
+             -4: "no HIP device", -5: "traversal stack too deep", -6: "unsupported"}
+    return names.get(code, f"status {code}")
+
+
+def env_threads() -> int:
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0)

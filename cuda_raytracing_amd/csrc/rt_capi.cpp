@@ -1,0 +1,269 @@
+// rt_capi.cpp — the C-ABI of include/rt_render.h over the HIP kernels.
+//
+// rt_render() is the drop-in for render()'s device half (raytracing.cu:1694-1771): compile + upload
+// the scene, seed per-pixel RNG (init_gpu_data, :1591-1606), run the render kernel (cuda_calc,
+// :1543-1589) and copy the framebuffer back.  rt_context_* keeps the scene resident in HBM for
+// repeated frames and multi-GPU shards.  Every failure is a status code; nothing exits.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "gpu_scene.h"
+#include "rt_kernels.h"
+#include "rt_render.h"
+#include "xorwow_jump.h"
+
+namespace {
+
+using rt::SceneImage;
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
+};
+
+struct DeviceGuard {   // restore the caller's current device
+  int prev = -1;
+  explicit DeviceGuard(int dev) { if (hipGetDevice(&prev) != hipSuccess) prev = -1; (void)hipSetDevice(dev); }
+  ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+int params_check(const rt_params *p) {
+  if (!p) return RT_ERR_INVALID_ARG;
+  if (p->width <= 0 || p->height <= 0 || p->samples_per_pixel <= 0) return RT_ERR_INVALID_ARG;
+  if (p->row_stride <= 0 || p->row_count < 0 || p->row_offset < 0) return RT_ERR_INVALID_ARG;
+  if (p->row_count > 0 &&
+      static_cast<int64_t>(p->row_offset) + static_cast<int64_t>(p->row_count - 1) * p->row_stride >= p->height)
+    return RT_ERR_INVALID_ARG;
+  if (static_cast<uint64_t>(p->row_count) * static_cast<uint64_t>(p->width) > 0x7fffffffull) return RT_ERR_INVALID_ARG;
+  if (static_cast<uint64_t>(p->height) * static_cast<uint64_t>(p->width) >= (1ull << 40)) return RT_ERR_INVALID_ARG;
+  return RT_OK;
+}
+
+}  // namespace
+
+struct rt_context {
+  int device = 0;
+  int cu_count = 0;
+  SceneImage img;
+  DevBuf scene, jump, rng, rc, work, counters;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  bool lds = false;
+  bool counted = false;
+  bool rendered = false;
+  uint64_t samples = 0;
+  size_t lds_bytes = 0;
+};
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char *rt_status_string(int s) {
+  switch (s) {
+    case RT_OK: return "ok";
+    case RT_ERR_INVALID_ARG: return "invalid argument";
+    case RT_ERR_SCENE: return "malformed scene";
+    case RT_ERR_HIP: return "HIP runtime error";
+    case RT_ERR_NO_DEVICE: return "no HIP device";
+    case RT_ERR_STACK: return "traversal stack too deep";
+    case RT_ERR_UNSUPPORTED: return "unsupported";
+  }
+  return "unknown status";
+}
+
+int rt_device_count(int *count) {
+  if (!count) return RT_ERR_INVALID_ARG;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return RT_OK;
+}
+
+void rt_context_destroy(rt_context *c) {
+  if (!c) return;
+  {
+    DeviceGuard g(c->device);
+    for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
+    c->scene.release(); c->jump.release(); c->rng.release(); c->rc.release();
+    c->work.release(); c->counters.release();
+  }
+  delete c;
+}
+
+int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
+  if (!scene || !out) return RT_ERR_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RT_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return RT_ERR_INVALID_ARG;
+  rt_context *c = new (std::nothrow) rt_context();
+  if (!c) return RT_ERR_INVALID_ARG;
+  c->device = device;
+  int st = rt::compile_scene(scene, &c->img);
+  if (st != RT_OK) { delete c; return st; }
+  while (c->img.words.size() % 4) c->img.words.push_back(0);
+  if (c->img.stack_need > 512) { delete c; return RT_ERR_STACK; }
+  DeviceGuard g(device);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_context_destroy(c); return RT_ERR_HIP; }
+  c->cu_count = prop.multiProcessorCount;
+  const std::vector<uint32_t> &J = rt::xorwow_jump_tables();
+  bool ok = c->scene.ensure(c->img.words.size() * 4) == hipSuccess &&
+            hipMemcpy(c->scene.p, c->img.words.data(), c->img.words.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            c->jump.ensure(J.size() * 4) == hipSuccess &&
+            hipMemcpy(c->jump.p, J.data(), J.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+            c->work.ensure(64) == hipSuccess &&
+            c->counters.ensure(RT_CNT__COUNT * sizeof(unsigned long long)) == hipSuccess;
+  for (hipEvent_t &e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+  if (!ok) { rt_context_destroy(c); return RT_ERR_HIP; }
+  *out = c;
+  return RT_OK;
+}
+
+int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, float *out_dev, void *stream) {
+  if (!c || !cam) return RT_ERR_INVALID_ARG;
+  int st = params_check(p);
+  if (st != RT_OK) return st;
+  if (!out_dev && p->row_count > 0) return RT_ERR_INVALID_ARG;
+  DeviceGuard g(c->device);
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const uint32_t n = static_cast<uint32_t>(p->row_count) * static_cast<uint32_t>(p->width);
+  const uint32_t mb = static_cast<uint8_t>(p->max_bounces);   // rc_stack.max_count is u8 (:220,1596)
+  c->counted = (p->flags & RT_FLAG_COUNT) != 0;
+  c->samples = static_cast<uint64_t>(n) * static_cast<uint64_t>(p->samples_per_pixel);
+  c->rendered = true;
+  if (n == 0) {
+    (void)hipEventRecord(c->ev[0], s); (void)hipEventRecord(c->ev[1], s); (void)hipEventRecord(c->ev[2], s);
+    return RT_OK;
+  }
+  if (mb == 0) {   // ray_color returns {0} without tracing (:1339): every pixel is exactly 0
+    (void)hipEventRecord(c->ev[0], s);
+    (void)hipEventRecord(c->ev[1], s);
+    if (hipMemsetAsync(out_dev, 0, static_cast<size_t>(n) * 12, s) != hipSuccess) return RT_ERR_HIP;
+    (void)hipEventRecord(c->ev[2], s);
+    return RT_OK;
+  }
+
+  // launch geometry: persistent grid = resident blocks per CU x CUs
+  c->lds = c->img.words.size() <= rt::kLdsSceneMaxWords && !(p->flags & RT_FLAG_GLOBAL_SCENE);
+  const uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
+  const size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * c->img.stack_need * 64 * 2;
+  c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + stack_bytes;
+  const int per_cu = rt::render_blocks_per_cu(c->lds, c->counted, c->lds_bytes);
+  uint64_t blocks = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(c->cu_count);
+  const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
+  blocks = std::max<uint64_t>(1, std::min(blocks, needed));
+  const uint32_t threads = static_cast<uint32_t>(blocks * rt::kBlock);
+
+  if (c->rng.ensure(static_cast<size_t>(n) * 6 * 4) != hipSuccess) return RT_ERR_HIP;
+  if (c->rc.ensure(static_cast<size_t>(mb) * 3 * threads * 4) != hipSuccess) return RT_ERR_HIP;
+
+  rt::SeedArgs sa{};
+  sa.jump = static_cast<const uint32_t *>(c->jump.p);
+  rt::xorwow_seed_base(p->seed, sa.base);
+  sa.width = p->width; sa.row_offset = p->row_offset; sa.row_stride = p->row_stride;
+  sa.n_pixels = n;
+  sa.per_thread = 64;
+  sa.rng = static_cast<uint32_t *>(c->rng.p);
+
+  rt::RenderArgs a{};
+  a.scene = static_cast<const uint32_t *>(c->scene.p);
+  a.scene_words = static_cast<uint32_t>(c->img.words.size());
+  a.off_mats = c->img.off_mats; a.off_texs = c->img.off_texs; a.off_perlin = c->img.off_perlin;
+  a.off_pixels = c->img.off_pixels;
+  a.pixel_words = static_cast<uint32_t>(c->img.words.size()) - c->img.off_pixels;
+  a.root = c->img.root;
+  a.stack_cap = c->img.stack_need;
+  a.stack_lds_word = scene_lds_words;
+  a.needs_uv = c->img.needs_uv ? 1u : 0u;
+  const rtr_vec3 *v3s[6] = {&cam->pixel00, &cam->delta_u, &cam->delta_v, &cam->center, &cam->defocus_u, &cam->defocus_v};
+  float *dst[6] = {a.p00, a.du, a.dv, a.center, a.dfu, a.dfv};
+  for (int k = 0; k < 6; ++k) { dst[k][0] = v3s[k]->x; dst[k][1] = v3s[k]->y; dst[k][2] = v3s[k]->z; }
+  a.defocus_angle = cam->defocus_angle;
+  a.width = p->width; a.row_offset = p->row_offset; a.row_stride = p->row_stride;
+  a.spp = p->samples_per_pixel;
+  a.max_bounces = static_cast<int32_t>(mb);
+  a.bg[0] = p->background.x; a.bg[1] = p->background.y; a.bg[2] = p->background.z;
+  a.sample_scale = 1.0f / static_cast<float>(p->samples_per_pixel);   // :1657
+  a.n_pixels = n;
+  a.rng = static_cast<const uint32_t *>(c->rng.p);
+  a.out = out_dev;
+  a.rc = static_cast<float *>(c->rc.p);
+  a.threads = threads;
+  a.work = static_cast<uint32_t *>(c->work.p);
+  a.counters = static_cast<unsigned long long *>(c->counters.p);
+
+  if (hipMemsetAsync(c->work.p, 0, 64, s) != hipSuccess) return RT_ERR_HIP;
+  if (c->counted && hipMemsetAsync(c->counters.p, 0, RT_CNT__COUNT * 8, s) != hipSuccess) return RT_ERR_HIP;
+  if (hipEventRecord(c->ev[0], s) != hipSuccess) return RT_ERR_HIP;
+  if (rt::launch_seed(sa, s) != hipSuccess) return RT_ERR_HIP;
+  if (hipEventRecord(c->ev[1], s) != hipSuccess) return RT_ERR_HIP;
+  if (rt::launch_render(a, c->lds, c->counted, static_cast<uint32_t>(blocks), c->lds_bytes, s) != hipSuccess)
+    return RT_ERR_HIP;
+  if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
+  return RT_OK;
+}
+
+int rt_context_timing(rt_context *c, rt_stats *st) {
+  if (!c || !st) return RT_ERR_INVALID_ARG;
+  std::memset(st, 0, sizeof *st);
+  st->stack_needed = static_cast<int32_t>(c->img.stack_need);
+  st->scene_in_lds = c->lds ? 1 : 0;
+  if (!c->rendered) return RT_OK;
+  DeviceGuard g(c->device);
+  if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;
+  float a = 0, b = 0;
+  if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) != hipSuccess) return RT_ERR_HIP;
+  if (hipEventElapsedTime(&b, c->ev[1], c->ev[2]) != hipSuccess) return RT_ERR_HIP;
+  st->init_ms = a;
+  st->render_ms = b;
+  st->samples = c->samples;
+  if (c->counted) {
+    unsigned long long h[RT_CNT__COUNT];
+    if (hipMemcpy(h, c->counters.p, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
+    for (int k = 0; k < RT_CNT__COUNT; ++k) st->counters[k] = h[k];
+  }
+  return RT_OK;
+}
+
+int rt_render(const rt_scene *scene, const rt_camera *cam, const rt_params *p, float *out_rgb, rt_stats *stats) {
+  auto t0 = std::chrono::steady_clock::now();
+  int st = params_check(p);
+  if (st != RT_OK) return st;
+  if (!scene || !cam || (!out_rgb && p->row_count > 0)) return RT_ERR_INVALID_ARG;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  rt_context *c = nullptr;
+  st = rt_context_create(scene, dev, &c);
+  if (st != RT_OK) return st;
+  const size_t bytes = static_cast<size_t>(p->row_count) * static_cast<size_t>(p->width) * 12;
+  DevBuf out;
+  {
+    DeviceGuard g(dev);
+    if (bytes && out.ensure(bytes) != hipSuccess) { rt_context_destroy(c); return RT_ERR_HIP; }
+    st = rt_context_render(c, cam, p, static_cast<float *>(out.p), nullptr);
+    if (st == RT_OK && hipDeviceSynchronize() != hipSuccess) st = RT_ERR_HIP;
+    if (st == RT_OK && bytes && hipMemcpy(out_rgb, out.p, bytes, hipMemcpyDeviceToHost) != hipSuccess) st = RT_ERR_HIP;
+    if (st == RT_OK && stats) st = rt_context_timing(c, stats);
+    out.release();
+  }
+  rt_context_destroy(c);
+  if (st == RT_OK && stats)
+    stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,30 @@
+// xorwow_jump.h — host-built jump tables for rocRAND-flavoured XORWOW subsequences.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+namespace rt {
+
+constexpr int kJumpPowers = 40;                 // subsequences < 2^40
+constexpr int kJumpMatrixWords = 160 * 5;       // rows[b][k]: image of unit vector e_b
+
+// P_k = A^(2^67 * 2^k), k in [0, kJumpPowers), concatenated (row-major [k][b][word]).
+const std::vector<uint32_t> &xorwow_jump_tables();
+
+// Seeded state {d, x0..x4} for (seed, subsequence) — same as rocrand_init(seed, subsequence, 0).
+void xorwow_seed_host(uint64_t seed, uint64_t subsequence, uint32_t state[6]);
+
+// rocRAND's constant seeding (rocrand_xorwow.h xorwow_engine ctor), no jump
+inline void xorwow_seed_base(uint64_t seed, uint32_t state[6]) {
+  uint32_t x[5] = {123456789u, 362436069u, 521288629u, 88675123u, 5783321u};
+  uint32_t d = 6615241u;
+  uint32_t s0 = static_cast<uint32_t>(seed) ^ 0x2c7f967fu;
+  uint32_t s1 = static_cast<uint32_t>(seed >> 32) ^ 0xa03697cbu;
+  uint32_t t0 = 1228688033u * s0, t1 = 2073658381u * s1;
+  x[0] += t0; x[1] ^= t0; x[2] += t1; x[3] ^= t1; x[4] += t0;
+  d += t1 + t0;
+  state[0] = d;
+  for (int k = 0; k < 5; ++k) state[1 + k] = x[k];
+}
+
+}  // namespace rt

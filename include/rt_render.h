@@ -1,0 +1,133 @@
+/*
+ * rt_render.h — C-ABI of the MI355X per-pixel render path (the drop-in boundary).
+ *
+ * Replaces, in luk-zm/cuda_raytracing:
+ *   - the device half of `void render(World*, RenderSettings*)` (src/raytracing.cu:1694-1771):
+ *     buffer allocation + H2D copies (1694-1744), `init_gpu_data` RNG seeding (1591-1606,1746),
+ *     the `cuda_calc` launch (1543-1589,1754) and the D2H framebuffer copy (1770-1771);
+ *   - the kernel argument list of `cuda_calc` (1543-1547), which becomes rt_camera + rt_params.
+ *
+ * The host keeps scene building, BVH construction, camera setup and PPM output (rt_host.h) and
+ * hands the reference's own scene buffers (layout: rt_ref_layout.h) across this boundary.
+ *
+ * Conventions (unlike the reference, which prints errors and returns void):
+ *   - every entry point returns RT_OK (0) or a negative RT_ERR_* code and never exits;
+ *   - all buffers are caller-owned; nothing is retained after return except inside an rt_context;
+ *   - thread-compatible: one call per context (or per device for rt_render) at a time.
+ * The CPU oracle (oracle/) exports the same signature as `rt_render_cpu` for parity tests.
+ */
+#ifndef RT_RENDER_H
+#define RT_RENDER_H
+
+#include <stdint.h>
+#include "rt_ref_layout.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* status codes */
+#define RT_OK                 0
+#define RT_ERR_INVALID_ARG   -1   /* null pointer, bad size, bad shard geometry */
+#define RT_ERR_SCENE         -2   /* malformed scene bytes (bad record kind, ref or texture offset) */
+#define RT_ERR_HIP           -3   /* HIP runtime failure (allocation, launch, copy) */
+#define RT_ERR_NO_DEVICE     -4   /* no HIP device visible */
+#define RT_ERR_STACK         -5   /* scene needs a deeper traversal stack than the kernel supports */
+#define RT_ERR_UNSUPPORTED   -6   /* feature outside this build */
+
+/* Scene bytes exactly as the reference builds them (raytracing.cu:1699-1733). */
+typedef struct rt_scene {
+  const rtr_hittable *hittables;   /* HittableList.objects[count]          (raytracing.cu:155-160) */
+  uint32_t hittable_count;
+  const uint16_t *refs;            /* HittableRefList.data: WorldRef -> record index (raytracing.cu:1-7) */
+  uint32_t ref_count;
+  uint16_t root;                   /* WorldRef of the root BVH node (SceneData.root_bvh_node, :234) */
+  uint16_t pad_;
+  const uint8_t *textures;         /* TextureList arena bytes [0, texture_bytes) (raytracing.cu:56-59) */
+  uint64_t texture_bytes;
+} rt_scene;
+
+/* Camera values `render()` computes on the host and passes to cuda_calc (raytracing.cu:1657-1692). */
+typedef struct rt_camera {
+  rtr_vec3 pixel00;        /* current_pixel_center: centre of pixel (0,0) (:1690-1692) */
+  rtr_vec3 delta_u;        /* pixel_delta_u (:1679) */
+  rtr_vec3 delta_v;        /* pixel_delta_v (:1678) */
+  rtr_vec3 center;         /* camera_pos = lookfrom (:1669) */
+  rtr_vec3 defocus_u;      /* defocus_disk_u (:1687) */
+  rtr_vec3 defocus_v;      /* defocus_disk_v (:1688) */
+  float defocus_angle;     /* settings.defocus_angle: > 0 enables the lens sample (:1571) */
+} rt_camera;
+
+/* Render parameters.  Rows rendered: row_offset + k*row_stride for k in [0, row_count).
+ * A full frame is {0, 1, height}; GPU g of G renders {g, G, ceil((height-g)/G)} (row-interleaved
+ * shards).  The RNG subsequence of pixel (i,j) is always the GLOBAL index i*width+j (:1604), so
+ * the image is bit-identical for any shard geometry. */
+typedef struct rt_params {
+  int32_t width, height;
+  int32_t row_offset, row_stride, row_count;
+  int32_t samples_per_pixel;       /* settings.samples_per_pixel (:1568) */
+  int32_t max_bounces;             /* settings.max_bounces, truncated to u8 like rc_stack.max_count (:220,1596) */
+  rtr_vec3 background;             /* settings.background_color (:1584) */
+  uint64_t seed;                   /* XORWOW seed; the reference uses 1234 (:1747) */
+  uint32_t flags;                  /* RT_FLAG_* */
+  uint32_t pad_;
+} rt_params;
+
+#define RT_FLAG_COUNT       0x1u   /* collect traversal/shading counters into rt_stats.counters */
+#define RT_FLAG_GLOBAL_SCENE 0x2u  /* keep the scene in global memory even when it fits in LDS */
+
+/* rt_stats.counters[] slots (filled only with RT_FLAG_COUNT) */
+enum {
+  RT_CNT_VISIT_SPHERE = 0, RT_CNT_VISIT_BVH, RT_CNT_VISIT_TRIANGLE, RT_CNT_VISIT_QUAD,
+  RT_CNT_VISIT_TRANSLATE, RT_CNT_VISIT_YROTATE, RT_CNT_VISIT_GROUP,
+  RT_CNT_BOUNCES,          /* scattering hits (pushes onto the colour stack) */
+  RT_CNT_SHADES,           /* closest-hit shading events (any material) */
+  RT_CNT_PERLIN,           /* Perlin turbulence evaluations */
+  RT_CNT_RNG_DRAWS,        /* uniform draws */
+  RT_CNT_SAMPLES,
+  RT_CNT_MAX_STACK,        /* deepest hit-stack use seen (max, not sum) */
+  RT_CNT_STACK_OVERFLOW,   /* traversals that would have overflowed (must be 0) */
+  RT_CNT__COUNT = 16
+};
+
+typedef struct rt_stats {
+  double init_ms;          /* RNG seeding kernel (reference: init_gpu_data, untimed there) */
+  double render_ms;        /* render kernel (the reference's "Rendering time" region, :1752-1768) */
+  double total_ms;         /* host wall time of the whole call */
+  uint64_t samples;        /* pixels * spp rendered by this call */
+  uint64_t counters[RT_CNT__COUNT];
+  int32_t stack_needed;    /* exact worst-case hit-stack depth of this scene */
+  int32_t scene_in_lds;    /* 1 if the compiled scene was staged in LDS */
+} rt_stats;
+
+/* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of
+ * row_count*width*3 floats (linear RGB, already scaled by 1/spp, row-major over the shard's rows).
+ * The drop-in for raytracing.cu:1694-1771. */
+int rt_render(const rt_scene *scene, const rt_camera *camera, const rt_params *params,
+              float *out_rgb, rt_stats *stats);
+
+/* Device-resident path: the scene stays in HBM across calls (bench / multi-GPU). */
+typedef struct rt_context rt_context;
+int rt_context_create(const rt_scene *scene, int device, rt_context **out);
+/* out_rgb_device: device buffer of row_count*width*3 floats.  stream: hipStream_t (NULL = null
+ * stream).  Asynchronous; timings are read with rt_context_timing() after the stream completes. */
+int rt_context_render(rt_context *ctx, const rt_camera *camera, const rt_params *params,
+                      float *out_rgb_device, void *stream);
+/* Blocks on the last render's events; fills init/render ms, samples and (if counted) counters. */
+int rt_context_timing(rt_context *ctx, rt_stats *stats);
+void rt_context_destroy(rt_context *ctx);
+
+const char *rt_status_string(int status);
+int rt_device_count(int *count);
+int rt_abi_version(void);
+
+/* CPU oracle (oracle/liboracle_rt.so) — test infrastructure only, same contract as rt_render. */
+int rt_render_cpu(const rt_scene *scene, const rt_camera *camera, const rt_params *params,
+                  float *out_rgb, rt_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_RENDER_H */
