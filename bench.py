@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the per-pixel render path on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scene 0] [--width 1920] [--height 1080]
+                    [--spp 512] [--bounces 16] [--no-cpu-baseline]
+
+A "step" is one frame: RNG seeding kernel + render kernel (+ the RCCL row gather to rank 0 when N>1),
+with the scene already resident in HBM.  Default workload = BASELINE config 2: scene 0 (fv1) at
+1920x1080, spp 512, depth 16 on one GPU.  With N ranks (torch.distributed.run, one process per GPU,
+backend "nccl" = RCCL) the frame grows to ~N x the pixels at the same aspect and camera (weak scaling)
+and rows are interleaved across ranks.  Rank 0 prints ONE JSON line.
+
+The printed value is samples of all ranks / max-over-ranks wall time of the K timed steps.
+roofline: VALU-bound kernel; achieved = algorithmic FP32 ops per render launch (op model of
+SURVEY §8d evaluated on this workload's measured per-sample visit counts) / the render kernel's mean
+HIP-event duration.  cpu_baseline: the C oracle on this host's cores over a bounded row sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch  # first: one HIP runtime per process (cuda_raytracing_amd._abi._bind_single_hip_runtime)
+import torch.distributed as dist
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+import cuda_raytracing_amd as rt  # noqa: E402
+from cuda_raytracing_amd import _abi  # noqa: E402
+from cuda_raytracing_amd.multi_gpu import gather_rows, weak_scaled_resolution  # noqa: E402
+
+# FP32 op weights per event (counted from the reference source, unfused, 1 op each)
+OP_WEIGHTS = {
+    "visit_sphere": 31, "visit_bvh": 24, "visit_triangle": 49, "visit_quad": 49,
+    "visit_translate": 3, "visit_yrotate": 12, "visit_group": 0,
+    "shades": 100, "perlin": 1500,
+}
+OPS_PER_SAMPLE_FIXED = 30                 # camera ray generation
+# non-packed FP32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (MI355X_MICROARCH.md: 157.3 TFLOPS
+# spec counts an FMA as 2; the path is compiled without contraction, so 1 op = 1 lane-instruction)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def op_model(counters: dict, samples: int) -> float:
+    ops = sum(OP_WEIGHTS[k] * counters[k] for k in OP_WEIGHTS) + OPS_PER_SAMPLE_FIXED * samples
+    return ops / max(samples, 1)
+
+
+def cpu_baseline(world, settings, W, H, spp, bounces, budget_s):
+    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample."""
+    import ctypes as C
+    import numpy as np
+    L = _abi.oracle_lib()
+    cam, W, H = rt.camera_from_settings(settings, W, H)
+    stride = 8
+    rows = len(range(0, H, stride))
+
+    def run(s):
+        p = rt.make_params(settings, W, H, spp=s, bounces=bounces, row_offset=0, row_stride=stride, row_count=rows)
+        out = np.zeros((rows, W, 3), np.float32)
+        st = _abi.Stats()
+        t = time.perf_counter()
+        rc = L.rt_render_cpu(C.byref(world.scene()), C.byref(cam), C.byref(p), out.ctypes.data_as(C.c_void_p),
+                             C.byref(st))
+        dt = time.perf_counter() - t
+        assert rc == 0, rc
+        return rows * W * s, dt
+
+    n, dt = run(2)                                   # calibration
+    rate = n / dt
+    s = int(max(2, min(spp, budget_s * rate / (rows * W))))
+    n, dt = run(s)
+    return {
+        "value": n / dt / 1e6, "unit": "Msamples/s", "cores": int(L.rt_oracle_threads()), "kind": "port",
+        "sample": f"scene rows 0::{stride} ({rows} rows x {W} px) at spp {s}, d{bounces}: {n:.3g} samples in {dt:.1f} s",
+    }
+
+
+def load_traffic(workload: str):
+    f = REPO / "profiles" / "hbm_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(workload)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", type=int, default=0)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=512)
+    ap.add_argument("--bounces", type=int, default=16)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle wall time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    # ---- host pre-pass (untimed, like the reference's make_bvh + camera) ----
+    world, settings = rt.build_scene(args.scene)
+    W, H = weak_scaled_resolution(args.width, args.height, world_size)
+    cam, W, H = rt.camera_from_settings(settings, W, H)
+    off, stride, rows = rt.shard_rows(H, rank, world_size)
+    params = rt.make_params(settings, W, H, spp=args.spp, bounces=args.bounces,
+                            row_offset=off, row_stride=stride, row_count=rows)
+    ctx = rt.RenderContext(world.scene(), device=local_rank)
+    stream = torch.cuda.current_stream()
+    out = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
+    workload = f"scene{args.scene}_{rt.scene_name(args.scene)}_{W}x{H}_spp{args.spp}_d{args.bounces}"
+
+    # ---- op model: per-sample event rates of THIS workload (counting variant, untimed) ----
+    model_spp = min(args.spp, 8)
+    pc = rt.make_params(settings, W, H, spp=model_spp, bounces=args.bounces,
+                        row_offset=off, row_stride=stride, row_count=rows, flags=rt.RT_FLAG_COUNT)
+    ctx.render_into(cam, pc, out.data_ptr(), stream.cuda_stream)
+    cst = ctx.timing()
+    counters = cst.counter_dict()
+    ops_per_sample = op_model(counters, counters["samples"])
+
+    def step():
+        ctx.render_into(cam, params, out.data_ptr(), stream.cuda_stream)
+        st = ctx.timing()                                     # waits on the frame's events
+        if world_size > 1:
+            gather_rows(out, H, W, rank, world_size)
+        return st
+
+    for _ in range(args.warmup):
+        step()
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    render_ms, init_ms = [], []
+    for _ in range(args.steps):
+        st = step()
+        render_ms.append(st.render_ms)
+        init_ms.append(st.init_ms)
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world_size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    samples_per_step = W * H * args.spp                  # all ranks together
+    value = samples_per_step * args.steps / elapsed / 1e6
+    mean_render_ms = sum(render_ms) / len(render_ms)
+    local_samples = rows * W * args.spp
+    achieved = ops_per_sample * local_samples / (mean_render_ms / 1e3) / 1e12
+
+    if rank == 0:
+        line = {
+            "metric": "Msamples/sec (pixels x spp / s) at 1920x1080 spp=512 d=16",
+            "value": round(value, 2),
+            "unit": "Msamples/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: reference scene catalog rebuilt on the host (glibc-rand seed 1), XORWOW seed 1234",
+            "config": {
+                "workload": workload,
+                "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
+                "parallelism": f"rows interleaved x{world_size}" + (" + RCCL gather" if world_size > 1 else ""),
+                "pixels_per_gpu": rows * W,
+            },
+            "kernel_ms": {"render_mean": round(mean_render_ms, 3), "seed_mean": round(sum(init_ms) / len(init_ms), 3)},
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved, 3),
+                "peak": round(VALU_PEAK_TOPS, 2),
+                "unit": "Tops/s",
+                "frac": round(achieved / VALU_PEAK_TOPS, 4),
+                "traffic": load_traffic(workload),
+                "ops_per_sample": round(ops_per_sample, 1),
+                "counters_per_sample": {k: round(v / max(counters["samples"], 1), 4) for k, v in counters.items()
+                                        if k not in ("samples", "max_stack", "stack_overflow", "rng_draws")},
+            },
+        }
+        if world_size == 1 and not args.no_cpu_baseline:
+            try:
+                line["cpu_baseline"] = cpu_baseline(world, settings, W, H, args.spp, args.bounces, args.cpu_budget)
+            except Exception as e:  # the baseline must never hide the GPU number
+                line["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,8 +10,6 @@ The render entry points call the HIP library only; a missing library is an error
 from __future__ import annotations
 
 import ctypes as C
-from dataclasses import dataclass
-
 import numpy as np
 
 from . import _abi
@@ -22,7 +20,7 @@ from ._abi import (Camera, Params, Scene, Settings, Stats, Vec3, vec3, RT_FLAG_C
 __all__ = [
     "World", "Camera", "Params", "Scene", "Settings", "Stats", "vec3", "build_scene",
     "camera_from_settings", "make_params", "render", "RenderContext", "tonemap", "write_ppm",
-    "scene_name", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
+    "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError",
 ]
 
@@ -166,6 +164,26 @@ class BlobScene:
         sc.texture_bytes = self.ntex
         sc._owner = self
         return sc
+
+
+def shard_rows(height: int, rank: int, world: int) -> tuple[int, int, int]:
+    """Row-interleaved shard of `rank` in `world`: (row_offset, row_stride, row_count).
+
+    Row r goes to GPU r mod G: interleaving balances the sky-heavy top rows against the
+    expensive ground rows.  The RNG subsequence is the global pixel index, so any sharding reproduces
+    the single-GPU image bit for bit."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError("bad shard geometry")
+    return rank, world, len(range(rank, height, world))
+
+
+def unshard(shards: list, height: int, width: int) -> np.ndarray:
+    """Inverse of shard_rows: list of [rows_k, W, 3] arrays (rank order) -> [H, W, 3]."""
+    world = len(shards)
+    img = np.empty((height, width, 3), dtype=np.float32)
+    for r, sh in enumerate(shards):
+        img[r::world] = sh
+    return img
 
 
 def build_scene(index: int, capacity: int | None = None):

@@ -206,6 +206,7 @@ def oracle_lib():
         _sig(L.rt_oracle_sinf, C.c_float, C.c_float)
         _sig(L.rt_oracle_pow5f, C.c_float, C.c_float)
         _sig(L.rt_oracle_uniforms, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int)
+        _sig(L.rt_oracle_threads, C.c_int)
         _oracle = L
     return _oracle
 

@@ -874,4 +874,12 @@ int rt_write_ppm(const char *path, const float *rgb, uint32_t width, uint32_t he
   return n == bytes.size() ? RT_OK : RT_ERR_INVALID_ARG;
 }
 
+int rt_abi_struct_sizes(uint32_t *out, int n) {
+  const uint32_t v[8] = {sizeof(rt_scene), sizeof(rt_camera), sizeof(rt_params), sizeof(rt_stats),
+                         sizeof(rt_settings), sizeof(rtr_hittable), sizeof(rtr_material), sizeof(rtr_texture)};
+  if (!out || n < 0) return RT_ERR_INVALID_ARG;
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  return 8;
+}
+
 }  // extern "C"

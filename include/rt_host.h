@@ -94,6 +94,10 @@ int rt_reference_stack_depth(const rt_scene *scene, uint32_t *depth);
 void rt_tonemap(const float *rgb, size_t pixels, uint8_t *out_rgb8);
 int rt_write_ppm(const char *path, const float *rgb, uint32_t width, uint32_t height);
 
+/* sizes of the ABI structs as compiled (bindings check their mirrors against these):
+ * [rt_scene, rt_camera, rt_params, rt_stats, rt_settings, rtr_hittable, rtr_material, rtr_texture] */
+int rt_abi_struct_sizes(uint32_t *out, int n);
+
 #ifdef __cplusplus
 }
 #endif

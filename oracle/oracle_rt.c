@@ -18,8 +18,8 @@
  * Documented substitutions (identical in the HIP kernel):
  *   - cuRAND XORWOW -> rocRAND XORWOW (seed salting + uniform mapping differ);
  *   - sinf in the noise texture (raytracing.cu:389) -> rt_sinf below: the float rounding of a
- *     double-precision sine with a fixed reduction + polynomial (faithful; matches glibc sinf on
- *     >99.99 % of inputs, tests/test_oracle.py);
+ *     double-precision sine with a fixed reduction + polynomial (correctly rounded on every tested
+ *     input; glibc's sinf agrees on ~98.7 %, CUDA's device sinf is within 2 ulp; tests/test_oracle.py);
  *   - powf(x, 5.0f) in Schlick's reflectance (raytracing.cu:436) -> (float)(x^5 in double).
  */
 #include <math.h>
@@ -713,4 +713,13 @@ int rt_oracle_uniforms(uint64_t seed, uint64_t subsequence, float *out, int n) {
   xw_init(seed, subsequence, &s);
   for (int i = 0; i < n; ++i) out[i] = uniform(&s, &cn);
   return RT_OK;
+}
+
+/* OpenMP threads rt_render_cpu will use (bench.py reports it as cpu_baseline.cores) */
+int rt_oracle_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
 }

@@ -1,0 +1,61 @@
+"""Multi-rank frame sharding + gather, world_size 2 over gloo on CPU.
+
+The GPU bench runs the same cuda_raytracing_amd.multi_gpu.gather_rows over RCCL; here each rank renders
+its row-interleaved shard with the CPU oracle (test infrastructure) and rank 0 checks the gathered
+frame against a single-process render bit for bit.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import REPO, bits, oracle_render
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, W, H, result):
+    sys.path.insert(0, str(REPO))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import cuda_raytracing_amd as rt
+    from cuda_raytracing_amd.multi_gpu import gather_rows
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    off, stride, cnt = rt.shard_rows(H, rank, world)
+    rc, shard, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=3, bounces=6, row_offset=off,
+                                                                 row_stride=stride, row_count=cnt))
+    assert rc == 0
+    img = gather_rows(torch.from_numpy(shard), H, W, rank, world)
+    if rank == 0:
+        rc, full, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=3, bounces=6))
+        result["equal"] = bool(np.array_equal(bits(img.numpy()), bits(full)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("H", [17, 18])
+def test_gather_rows_world2(H):
+    mgr = mp.Manager()
+    result = mgr.dict()
+    mp.spawn(_worker, args=(2, _free_port(), 24, H, result), nprocs=2, join=True)
+    assert result.get("equal") is True
+
+
+def test_weak_scaled_resolution():
+    from cuda_raytracing_amd.multi_gpu import weak_scaled_resolution
+    assert weak_scaled_resolution(1920, 1080, 1) == (1920, 1080)
+    assert weak_scaled_resolution(1920, 1080, 4) == (3840, 2160)
+    W, H = weak_scaled_resolution(1920, 1080, 8)
+    assert abs(W * H / (1920 * 1080) - 8) < 0.01

@@ -1,0 +1,174 @@
+"""HIP render path vs the CPU oracle and the golden fixtures — bit-exact (MI355X only).
+
+Tolerance: none.  Every case compares the float32 framebuffer bit patterns.  All GPU work goes through
+the C-ABI (librt_hip.so); the oracle is only the checker.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import torch  # noqa: F401  one HIP runtime per process (see cuda_raytracing_amd._abi)
+
+import cuda_raytracing_amd as rt
+from cuda_raytracing_amd import _abi
+from conftest import bits, blob_scene, camera_from_manifest, oracle_render, params_for
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    n = C.c_int()
+    _abi.hip_lib().rt_device_count(C.byref(n))
+    assert n.value > 0, "no HIP device: the GPU tests must run on an MI355X (no CPU fallback exists)"
+
+
+def gpu(sc, cam, p):
+    return rt.render(sc, cam, p, with_stats=True)
+
+
+def test_golden_frames(manifest, golden_frames, golden_scenes):
+    for case in manifest["cases"]:
+        idx = case["scene"]
+        if f"s{idx}_hittables" in golden_scenes:
+            sc = blob_scene(golden_scenes, idx).scene()
+        else:
+            w, _ = rt.build_scene(idx)
+            sc = w.scene()
+        fb, st = gpu(sc, camera_from_manifest(case), params_for(case, manifest))
+        assert np.array_equal(bits(fb), bits(golden_frames[case["name"] + "_fb"])), case["name"]
+        assert np.array_equal(rt.tonemap(fb), golden_frames[case["name"] + "_u8"])
+
+
+@pytest.mark.parametrize("idx", list(range(rt.RT_SCENE_COUNT)))
+def test_every_catalog_scene_vs_oracle(idx):
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 24, 16)
+    p = rt.make_params(s, W, H, spp=3, bounces=min(s.max_bounces, 50))
+    fb, _ = gpu(w.scene(), cam, p)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    assert np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("idx,W,H,spp,b", [(0, 96, 54, 8, 16), (1, 40, 40, 8, 50), (17, 64, 36, 4, 50),
+                                          (2, 48, 27, 4, 16), (20, 48, 27, 2, 16)])
+def test_counters_equal_oracle(idx, W, H, spp, b):
+    # same traversal, same shading events: the per-kind visit counts must match exactly
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_COUNT)
+    fb, st = gpu(w.scene(), cam, p)
+    rc, ref, ost = oracle_render(w.scene(), cam, p)
+    assert np.array_equal(bits(fb), bits(ref))
+    g, o = st.counter_dict(), ost.counter_dict()
+    for k in ("visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate", "visit_yrotate",
+              "visit_group", "bounces", "shades", "perlin", "samples"):
+        assert g[k] == o[k], (k, g[k], o[k])
+    assert g["max_stack"] <= st.stack_needed and g["stack_overflow"] == 0
+    assert o["max_stack"] <= st.stack_needed
+
+
+@pytest.mark.parametrize("idx", [0, 1, 17])
+def test_lds_and_global_scene_agree(idx):
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 48, 32)
+    p = rt.make_params(s, W, H, spp=4, bounces=16)
+    a, sa = gpu(w.scene(), cam, p)
+    p.flags = rt.RT_FLAG_GLOBAL_SCENE
+    b, sb = gpu(w.scene(), cam, p)
+    assert sa.scene_in_lds == 1 and sb.scene_in_lds == 0
+    assert np.array_equal(bits(a), bits(b))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_row_shards_reassemble(world):
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 70, 41)
+    full, _ = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=4, bounces=8))
+    shards = []
+    for r in range(world):
+        off, stride, cnt = rt.shard_rows(H, r, world)
+        shards.append(gpu(w.scene(), cam, rt.make_params(s, W, H, spp=4, bounces=8, row_offset=off,
+                                                         row_stride=stride, row_count=cnt))[0])
+    assert np.array_equal(bits(rt.unshard(shards, H, W)), bits(full))
+
+
+def test_edge_sizes_and_params():
+    w, s = rt.build_scene(0)
+    sc = w.scene()
+    for W, H, spp, b in [(1, 1, 1, 1), (1, 7, 3, 4), (65, 1, 2, 4), (63, 2, 5, 40), (129, 3, 1, 255)]:
+        cam, W2, H2 = rt.camera_from_settings(s, W, H)
+        p = rt.make_params(s, W2, H2, spp=spp, bounces=b)
+        fb, _ = gpu(sc, cam, p)
+        rc, ref, _ = oracle_render(sc, cam, p)
+        assert rc == 0 and np.array_equal(bits(fb), bits(ref)), (W, H, spp, b)
+    cam, W, H = rt.camera_from_settings(s, 16, 9)
+    for b in (0, 256):       # u8 max_count: no tracing at all -> exact zeros
+        fb, _ = gpu(sc, cam, rt.make_params(s, W, H, spp=2, bounces=b))
+        assert not fb.any() and not np.signbit(fb).any()
+    empty, _ = gpu(sc, cam, rt.make_params(s, W, H, spp=2, bounces=4, row_count=0))
+    assert empty.shape == (0, W, 3)
+    for bad in (dict(spp=0), dict(row_offset=9), dict(row_stride=0)):
+        p = rt.make_params(s, W, H, spp=bad.get("spp", 2), bounces=4)
+        if "row_offset" in bad:
+            p.row_offset = bad["row_offset"]
+        if "row_stride" in bad:
+            p.row_stride = bad["row_stride"]
+        with pytest.raises(rt.RenderError) as e:
+            gpu(sc, cam, p)
+        assert e.value.code == _abi.RT_ERR_INVALID_ARG
+
+
+def test_malformed_scenes_are_rejected():
+    w, s = rt.build_scene(0)
+    b = w.blobs()
+    cam, W, H = rt.camera_from_settings(s, 8, 8)
+    p = rt.make_params(s, W, H, spp=1, bounces=4)
+
+    def attempt(rec, refs, tex, root):
+        with pytest.raises(rt.RenderError) as e:
+            rt.render(rt.BlobScene(rec, refs, tex, root).scene(), cam, p)
+        assert e.value.code == _abi.RT_ERR_SCENE
+
+    rec = bytearray(b["hittables"])
+    rec[0:4] = (9).to_bytes(4, "little")                       # unknown record kind
+    attempt(bytes(rec), b["refs"], b["textures"], b["root"])
+    refs = b["refs"].copy()
+    refs[0] = 60000                                            # WorldRef to a missing record
+    attempt(b["hittables"], refs, b["textures"], b["root"])
+    attempt(b["hittables"], b["refs"], b["textures"][:40], b["root"])   # texture offsets past the arena
+    attempt(b["hittables"], b["refs"], b["textures"], 99)      # root beyond the ref list
+
+
+def test_full_size_rows_match_oracle():
+    # BASELINE config 2 geometry (1920x1080, d16) at reduced spp: three full-width rows from the GPU
+    # frame must equal the oracle's rendering of the same rows (shard-invariant RNG)
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 1920, 1080)
+    full, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=4, bounces=16))
+    again, _ = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=4, bounces=16))
+    assert np.array_equal(bits(full), bits(again))                    # deterministic
+    p = rt.make_params(s, W, H, spp=4, bounces=16, row_offset=1, row_stride=539, row_count=3)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(full[1::539][:3]), bits(ref))
+    assert np.isfinite(full).all() and (full >= 0).all()
+
+
+def test_context_reuse_and_torch_buffers():
+    w, s = rt.build_scene(17)
+    cam, W, H = rt.camera_from_settings(s, 40, 30)
+    ctx = rt.RenderContext(w.scene(), 0)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    for spp in (2, 5, 2):
+        p = rt.make_params(s, W, H, spp=spp, bounces=20)
+        ctx.render_into(cam, p, out.data_ptr(), stream.cuda_stream)
+        st = ctx.timing()
+        assert st.render_ms > 0 and st.samples == W * H * spp
+        ref, _ = gpu(w.scene(), cam, p)
+        assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
+    ctx.close()
