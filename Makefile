@@ -23,8 +23,10 @@ HIP_FLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno
 ORACLE_FLAGS := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -fopenmp -Wall -Wextra
 
 HOST_SRC := $(CSRC)/host/rt_host.cpp
-HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp
-HIP_HDR  := $(wildcard $(CSRC)/*.h) include/rt_render.h include/rt_ref_layout.h
+HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp \
+            $(CSRC)/scene_codegen.cpp $(CSRC)/rt_jit.cpp
+HIP_HDR  := $(wildcard $(CSRC)/*.h) $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h \
+            $(CSRC)/device/embedded_headers.inc include/rt_render.h include/rt_ref_layout.h
 
 all: host hip oracle cli
 
@@ -33,13 +35,17 @@ hip: $(LIBDIR)/librt_hip.so
 oracle: oracle/_build/liboracle_rt.so
 cli: bin/raytracing
 
-$(LIBDIR)/librt_host.so: $(HOST_SRC) $(CSRC)/host/glibc_rand.h include/rt_host.h include/rt_ref_layout.h
+$(LIBDIR)/librt_host.so: $(HOST_SRC) $(CSRC)/host/glibc_rand.h include/rt_host.h include/rt_ref_layout.h include/rt_render.h
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOST_FLAGS) $(INC) -shared $(HOST_SRC) -o $@
 
+# device headers embedded as text for the run-time (hipRTC) scene-specialised kernels
+$(CSRC)/device/embedded_headers.inc: $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h tools/embed_headers.py
+	python3 tools/embed_headers.py $@ kEmbedLayout=$(CSRC)/device/rt_layout.h kEmbedBody=$(CSRC)/device/rt_body.h
+
 $(LIBDIR)/librt_hip.so: $(HIP_SRC) $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIP_FLAGS) $(INC) -shared $(HIP_SRC) -o $@
+	$(HIPCC) $(HIP_FLAGS) $(INC) -shared $(HIP_SRC) -o $@ -L$(ROCM)/lib -lhiprtc
 
 oracle/_build/liboracle_rt.so: oracle/oracle_rt.c include/rt_render.h include/rt_ref_layout.h
 	@mkdir -p oracle/_build

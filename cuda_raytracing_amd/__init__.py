@@ -14,13 +14,16 @@ import numpy as np
 
 from . import _abi
 from ._abi import (Camera, Params, Scene, Settings, Stats, Vec3, vec3, RT_FLAG_COUNT,
-                   RT_FLAG_GLOBAL_SCENE, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
+                   RT_FLAG_GLOBAL_SCENE, RT_FLAG_NO_JIT, RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET,
+                   RT_FLAG_FORCE_STATIC, RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
                    RT_XF_TRANSLATE, RT_XF_YROTATE, RT_XF_YROTATE_TRANSLATE)
 
 __all__ = [
     "World", "Camera", "Params", "Scene", "Settings", "Stats", "vec3", "build_scene",
     "camera_from_settings", "make_params", "render", "RenderContext", "tonemap", "write_ppm",
-    "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
+    "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE",
+    "RT_FLAG_NO_JIT", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_TRAV_LANE",
+    "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError",
 ]
 
@@ -248,6 +251,11 @@ class RenderContext:
         _check(self._L.rt_context_timing(self._h, C.byref(st)), "rt_context_timing")
         return st
 
+    def note(self) -> str:
+        """Why the last render did not use the scene-specialised traversal ("" if it did)."""
+        n = self._L.rt_context_note(self._h)
+        return n.decode() if n else ""
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._L.rt_context_destroy(self._h)
@@ -255,6 +263,24 @@ class RenderContext:
 
     def __del__(self):
         self.close()
+
+
+def static_source(scene: Scene, max_visits: int = 256) -> tuple[str, int]:
+    """(hipRTC source of the scene-specialised traversal, node visits); RenderError over budget."""
+    buf = C.create_string_buffer(1 << 22)
+    v = C.c_uint32()
+    _check(_abi.hip_lib().rt_static_source(C.byref(scene), max_visits, buf, len(buf), C.byref(v)),
+           "rt_static_source")
+    return buf.value.decode(), v.value
+
+
+def static_compile(scene: Scene, arch: str = "gfx950", max_visits: int = 256) -> str:
+    """Compile the scene-specialised kernels with hipRTC (no device needed); returns the log."""
+    log = C.create_string_buffer(1 << 16)
+    rc = _abi.hip_lib().rt_static_compile(C.byref(scene), max_visits, arch.encode(), log, len(log))
+    if rc != 0:
+        raise RenderError(rc, "rt_static_compile: " + log.value.decode(errors="replace")[:4000])
+    return log.value.decode(errors="replace")
 
 
 def tonemap(rgb: np.ndarray) -> np.ndarray:

@@ -26,6 +26,9 @@ RT_ERR_UNSUPPORTED = -6
 
 RT_FLAG_COUNT = 0x1
 RT_FLAG_GLOBAL_SCENE = 0x2
+RT_FLAG_NO_JIT = 0x4
+RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET, RT_FLAG_FORCE_STATIC = 0x8, 0x10, 0x20
+RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC = 0, 1, 2
 
 CNT_NAMES = [
     "visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate",
@@ -86,6 +89,7 @@ class Stats(C.Structure):
         ("init_ms", C.c_double), ("render_ms", C.c_double), ("total_ms", C.c_double),
         ("samples", C.c_uint64), ("counters", C.c_uint64 * 16),
         ("stack_needed", C.c_int32), ("scene_in_lds", C.c_int32),
+        ("traversal", C.c_int32), ("jit_visits", C.c_int32),
     ]
 
     def counter_dict(self):
@@ -154,7 +158,8 @@ def host_lib():
 
 
 HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_timing",
-               "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version"]
+               "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
+               "rt_static_source", "rt_static_compile", "rt_context_note"]
 
 
 def _bind_single_hip_runtime():
@@ -190,6 +195,11 @@ def hip_lib():
         _sig(L.rt_status_string, C.c_char_p, C.c_int)
         _sig(L.rt_device_count, C.c_int, C.POINTER(C.c_int))
         _sig(L.rt_abi_version, C.c_int)
+        _sig(L.rt_static_source, C.c_int, C.POINTER(Scene), C.c_uint32, C.c_char_p, C.c_uint64,
+             C.POINTER(C.c_uint32))
+        _sig(L.rt_static_compile, C.c_int, C.POINTER(Scene), C.c_uint32, C.c_char_p, C.c_char_p,
+             C.c_uint64)
+        _sig(L.rt_context_note, C.c_char_p, P)
         _hip = L
     return _hip
 

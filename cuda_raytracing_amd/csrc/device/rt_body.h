@@ -1,0 +1,742 @@
+// rt_body.h — device code of the per-pixel render path (gfx950).
+//
+// Replaces cuda_calc (raytracing.cu:1543-1589) + ray_color (:1333-1371) + hit (:1079-1251) +
+// materials/textures/Perlin (:356-502, perlin_noise.cpp).  Compiled twice: offline by hipcc
+// (rt_device.hip: generic per-lane / packet traversal) and at run time by hipRTC (rt_jit.cpp: the
+// traversal of one specific scene expanded into straight-line code).  It therefore includes nothing
+// but rt_layout.h; the including translation unit provides the HIP device runtime.
+//
+// Arithmetic is the reference's, op for op: built with -ffp-contract=off and correctly rounded f32
+// divide/sqrt, ternary MIN/MAX semantics, the same RNG draw order — bit-exact against the oracle.
+#pragma once
+#include "rt_layout.h"
+
+namespace rt {
+
+extern __shared__ uint32_t g_lds[];   // [scene image (LDS variant)] [per-lane traversal stacks]
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 scale(float s, f3 v) { return mk(v.x * s, v.y * s, v.z * s); }
+__device__ __forceinline__ f3 flip(f3 v) { return mk(-v.x, -v.y, -v.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
+__device__ __forceinline__ f3 unit(f3 v) {              // vec3.h:106-114 (three divisions)
+  float l = length(v);
+  if (l == 0.0f) return mk(0.0f, 0.0f, 0.0f);
+  return mk(v.x / l, v.y / l, v.z / l);
+}
+__device__ __forceinline__ f3 line_at(f3 o, float t, f3 d) { return add(o, scale(t, d)); }
+__device__ __forceinline__ float tmin_(float a, float b) { return (a < b) ? a : b; }   // utility.h:6
+__device__ __forceinline__ float tmax_(float a, float b) { return (a < b) ? b : a; }   // utility.h:7
+__device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
+
+// |denom| >= 1e-8 (a double literal, raytracing.cu:1064) <=> |denom| >= the smallest float >= 1e-8
+constexpr float kDenomEps = 1.00000008274037099e-08f;   // 0x322BCC78
+static_assert(kDenomEps > 1e-8 && (kDenomEps - 1e-8) < 1e-15, "denominator threshold");
+constexpr float kTmin = 0.001f;                          // ray_tmin (raytracing.cu:1341)
+
+// ---------------------------------------------------------------------------------------------
+// scene memory: one word image, either in LDS or in HBM (read-only)
+// ---------------------------------------------------------------------------------------------
+template <bool LDS>
+struct Mem {
+  const uint32_t *__restrict__ g;
+  __device__ __forceinline__ uint32_t w(uint32_t i) const { return LDS ? g_lds[i] : g[i]; }
+  __device__ __forceinline__ float f(uint32_t i) const { return asf(w(i)); }
+  __device__ __forceinline__ uint4 w4(uint32_t i) const {   // i % 4 == 0
+    return LDS ? *reinterpret_cast<const uint4 *>(&g_lds[i]) : *reinterpret_cast<const uint4 *>(&g[i]);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t word_base, uint32_t b) const {
+    return LDS ? reinterpret_cast<const uint8_t *>(&g_lds[word_base])[b]
+               : reinterpret_cast<const uint8_t *>(&g[word_base])[b];
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// RNG: rocRAND XORWOW (replaces cuRAND)
+// ---------------------------------------------------------------------------------------------
+struct Rng {
+  uint32_t d, x0, x1, x2, x3, x4;
+  __device__ __forceinline__ uint32_t next() {
+    uint32_t t = x0 ^ (x0 >> 2);
+    x0 = x1; x1 = x2; x2 = x3; x3 = x4;
+    x4 = (x4 ^ (x4 << 4)) ^ (t ^ (t << 1));
+    d += 362437u;
+    return d + x4;
+  }
+  __device__ __forceinline__ float uniform() {       // rocrand_uniform: (0, 1]
+    const float inv = 2.3283064e-10f;
+    return inv + (static_cast<float>(next()) * inv);
+  }
+  __device__ __forceinline__ float bound(float lo, float hi) { return lo + (hi - lo) * uniform(); }
+};
+
+// sinf substitute (identical algorithm in the oracle: float rounding of a double sine)
+__device__ __forceinline__ float rt_sinf(float xf) {
+  double x = static_cast<double>(xf);
+  if (!(fabs(x) < 1.0e6)) return static_cast<float>(sin(x));
+  const double two_over_pi = 6.36619772367581382433e-01;
+  const double p1 = 1.57079632673412561417e+00;
+  const double p2 = 6.07710050630396597660e-11;
+  const double p3 = 2.02226624871116645580e-21;
+  double k = floor(x * two_over_pi + 0.5);
+  double r = ((x - k * p1) - k * p2) - k * p3;
+  long q = static_cast<long>(k) & 3;
+  double r2 = r * r;
+  double s = r + r * r2 * (-1.66666666666666666667e-01 + r2 * (8.33333333333333333333e-03 +
+             r2 * (-1.98412698412698412698e-04 + r2 * (2.75573192239858906526e-06 +
+             r2 * (-2.50521083854417187751e-08 + r2 * (1.60590438368216145994e-10 +
+             r2 * (-7.64716373181981647590e-13 + r2 * 2.81145725434552076320e-15)))))));
+  double c = 1.0 + r2 * (-0.5 + r2 * (4.16666666666666666667e-02 + r2 * (-1.38888888888888888889e-03 +
+             r2 * (2.48015873015873015873e-05 + r2 * (-2.75573192239858906526e-07 +
+             r2 * (2.08767569878680989792e-09 + r2 * (-1.14707455977297247139e-11 +
+             r2 * 4.77947733238738529744e-14)))))));
+  double res = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+  return static_cast<float>(res);
+}
+
+__device__ __forceinline__ float rt_pow5f(float xf) {   // powf(x, 5.0f) substitute
+  double x = static_cast<double>(xf);
+  double x2 = x * x;
+  double x4 = x2 * x2;
+  return static_cast<float>(x4 * x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// textures + Perlin (raytracing.cu:343-398, perlin_noise.cpp:1-46,72-85)
+// ---------------------------------------------------------------------------------------------
+template <bool LDS>
+__device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
+  float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
+  float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+  int32_t i = static_cast<int32_t>(fx), j = static_cast<int32_t>(fy), k = static_cast<int32_t>(fz);
+  const uint32_t pb = tb + 1024;   // perm_x bytes
+  uint32_t pi0 = S.byte(pb, i & 255), pi1 = S.byte(pb, (i + 1) & 255);
+  uint32_t pj0 = S.byte(pb, j & 255), pj1 = S.byte(pb, (j + 1) & 255);
+  uint32_t pk0 = S.byte(pb, k & 255), pk1 = S.byte(pb, (k + 1) & 255);
+  float uu = u * u * (3 - 2 * u);
+  float vv = v * v * (3 - 2 * v);
+  float ww = w * w * (3 - 2 * w);
+  // (a*uu + (1-a)*(1-uu)) is exactly uu or 1-uu for every finite uu (and NaN either way)
+  float wu[2] = {1 - uu, uu}, wv[2] = {1 - vv, vv}, wwk[2] = {1 - ww, ww};
+  float du[2] = {u, u - 1.0f}, dv[2] = {v, v - 1.0f}, dw[2] = {w, w - 1.0f};
+  uint32_t pi[2] = {pi0, pi1}, pj[2] = {pj0, pj1}, pk[2] = {pk0, pk1};
+  float accum = 0.0f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        uint32_t g = (pi[a] ^ pj[b] ^ pk[c]) & 255;
+        uint4 gr = S.w4(tb + 4 * g);
+        f3 grad = mk(asf(gr.x), asf(gr.y), asf(gr.z));
+        accum += wu[a] * wv[b] * wwk[c] * dot(grad, mk(du[a], dv[b], dw[c]));
+      }
+  return accum;
+}
+
+template <bool LDS, bool COUNT, bool NOISE, bool UV>
+__device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti, float u, float v, f3 p,
+                            uint32_t &perlin_count) {
+  for (int guard = 0; guard < 64; ++guard) {
+    const uint32_t b = A.off_texs + ti * kTexWords;
+    uint4 t0 = S.w4(b);
+    switch (t0.x) {
+      case T_SOLID:
+        return mk(asf(t0.y), asf(t0.z), asf(t0.w));
+      case T_CHECKER: {
+        float inv = asf(t0.w);
+        int32_t x = static_cast<int32_t>(floorf(inv * p.x));
+        int32_t y = static_cast<int32_t>(floorf(inv * p.y));
+        int32_t z = static_cast<int32_t>(floorf(inv * p.z));
+        bool even = ((x + y + z) & 1) == 0;
+        ti = even ? t0.y : t0.z;
+      } break;
+      case T_IMAGE: {
+        if (!UV) return mk(1, 0, 1);        // no pixels anywhere in the scene (host-checked)
+        uint4 t1 = S.w4(b + 4);
+        if (t1.x == 0) return mk(1, 0, 1);
+        int32_t wd = static_cast<int32_t>(t0.y), ht = static_cast<int32_t>(t0.z);
+        float cu = (u < 0) ? 0 : ((u > 1) ? 1 : u);
+        float cv = 1.0f - ((v < 0) ? 0 : ((v > 1) ? 1 : v));
+        int32_t x = static_cast<int32_t>(cu * wd), y = static_cast<int32_t>(cv * ht);
+        x = (x < 0) ? 0 : ((x > wd) ? wd : x);
+        y = (y < 0) ? 0 : ((y > ht) ? ht : y);
+        uint64_t wo = static_cast<uint64_t>(t0.w) + 3ull * (static_cast<uint64_t>(y) * wd + x);
+        if (wo + 3 > A.pixel_words) return mk(0, 0, 0);
+        uint32_t o = A.off_pixels + static_cast<uint32_t>(wo);
+        return mk(S.f(o), S.f(o + 1), S.f(o + 2));
+      }
+      case T_NOISE: {
+        if (!NOISE) return mk(0, 0, 0);     // unreachable: the host selects a NOISE variant
+        if (COUNT) perlin_count++;
+        const uint32_t tb = A.off_perlin + t0.y * kPerlinWords;
+        float accum = 0.0f, weight = 1.0f;
+        f3 q = p;
+        for (int oct = 0; oct < 7; ++oct) {
+          accum += weight * perlin_noise(S, tb, q);
+          weight *= 0.5f;
+          q = mk(q.x * 2, q.y * 2, q.z * 2);
+        }
+        float turb = fabsf(accum);
+        float s = 1 + rt_sinf(asf(t0.w) * p.z + 10 * turb);
+        return mk(0.5f * s, 0.5f * s, 0.5f * s);
+      }
+      default:
+        return mk(0, 0, 0);
+    }
+  }
+  return mk(0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// traversal state and the per-node operations of hit() (raytracing.cu:1079-1251)
+// ---------------------------------------------------------------------------------------------
+struct Ray { f3 o, d; float time; };
+struct Hit { f3 p, n; float t, u, v; uint32_t mat; bool front; };
+struct Visits { uint32_t k[7]; uint32_t max_sp; };
+
+// locals of hit() (:1082-1088) plus a cached 1/dir
+struct Trav {
+  f3 inv;          // 1/dir, refreshed whenever the ray direction changes (y-rotation enter/exit)
+  float tmax;      // shrinking ray_tmax (closest hit so far)
+  int sp;          // per-lane hit-stack depth (0 = traversal finished)
+  int tc, yc;      // translation / y-rotation cleanup counters
+  bool was_last, result;
+};
+
+__device__ __forceinline__ void trav_reset(Trav &T, const Ray &r) {
+  T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  T.tmax = __builtin_huge_valf();
+  T.sp = 0;
+  T.tc = 0; T.yc = 0;
+  T.was_last = false; T.result = false;
+}
+
+// aabb_hit (:990-1025) with the cached 1/dir; the three early returns folded into one flag
+__device__ __forceinline__ bool box_hit(const Trav &T, const Ray &r, float x0, float x1, float y0, float y1,
+                                        float z0, float z1) {
+  float t0 = kTmin, t1 = T.tmax;
+  float a = (x0 - r.o.x) * T.inv.x, c = (x1 - r.o.x) * T.inv.x;
+  if (T.inv.x < 0.0f && a > c) { float s = a; a = c; c = s; }
+  t0 = tmax_(t0, a); t1 = tmin_(t1, c);
+  bool miss = t1 <= t0;
+  a = (y0 - r.o.y) * T.inv.y; c = (y1 - r.o.y) * T.inv.y;
+  if (T.inv.y < 0.0f && a > c) { float s = a; a = c; c = s; }
+  t0 = tmax_(t0, a); t1 = tmin_(t1, c);
+  miss |= t1 <= t0;
+  a = (z0 - r.o.z) * T.inv.z; c = (z1 - r.o.z) * T.inv.z;
+  if (T.inv.z < 0.0f && a > c) { float s = a; a = c; c = s; }
+  t0 = tmax_(t0, a); t1 = tmin_(t1, c);
+  miss |= t1 <= t0;
+  return !miss;
+}
+
+// triangle / quad branch (:1131-1175) over geom_calc_hit (:1060-1077); in_xf: inside a transform
+__device__ __forceinline__ void planar_hit(Trav &T, const Ray &r, Hit &h, bool tri, uint32_t mat, f3 n, float dd,
+                                           f3 q, f3 uu, f3 vv, f3 ww, bool in_xf) {
+  float denom = dot(n, r.d);
+  if (fabsf(denom) >= kDenomEps) {
+    float t = (dd - dot(n, r.o)) / denom;
+    if (kTmin <= t && t <= T.tmax) {
+      f3 p = line_at(r.o, t, r.d);
+      f3 pq = sub(p, q);
+      float alpha = dot(ww, cross(pq, vv));
+      float beta = dot(ww, cross(uu, pq));
+      bool inside = (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
+      if (tri) inside = inside && (alpha + beta <= 1.0f);
+      if (inside) {
+        h.u = alpha; h.v = beta; h.t = t; h.p = p; h.mat = mat;
+        h.front = dot(r.d, n) < 0;
+        h.n = h.front ? n : flip(n);
+        T.tmax = t;
+        T.result = true;
+        if (in_xf) T.was_last = true;
+      }
+    }
+  }
+}
+
+// sphere branch (:1093-1123) + sphere_get_uv (:583-590, image textures only)
+template <bool UV>
+__device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
+                                           float inv_rad, bool in_xf) {
+  f3 center = line_at(c0, r.time, mv);
+  f3 oc = sub(center, r.o);
+  float a = dot(r.d, r.d);
+  float b = -2.0f * dot(r.d, oc);
+  float c = dot(oc, oc) - rad2;
+  float disc = b * b - 4 * a * c;
+  if (disc >= 0) {
+    float sq = sqrtf(disc);
+    float root = (-b - sq) / (2.0f * a);
+    if (kTmin >= root || root >= T.tmax) root = (-b + sq) / (2.0f * a);
+    if (kTmin < root && root < T.tmax) {
+      h.t = root;
+      h.p = line_at(r.o, root, r.d);
+      h.mat = mat;
+      f3 outward = scale(inv_rad, sub(h.p, center));
+      if (UV) {
+        const float pi = 3.1415926535897932385f;
+        float theta = acosf(-outward.y);
+        float phi = atan2f(-outward.z, outward.x) + pi;
+        h.u = phi / (2 * pi);
+        h.v = theta / pi;
+      }
+      h.front = dot(r.d, outward) < 0;
+      h.n = h.front ? outward : flip(outward);
+      T.tmax = h.t;
+      T.result = true;
+      if (in_xf) T.was_last = true;
+    }
+  }
+}
+
+// translation enter / cleanup (:1176-1191)
+__device__ __forceinline__ void translate_enter(Trav &T, Ray &r, f3 off) {
+  T.was_last = false;
+  r.o = sub(r.o, off);
+}
+__device__ __forceinline__ void translate_exit(Trav &T, Ray &r, Hit &h, f3 off) {
+  r.o = add(r.o, off);
+  if (T.was_last) h.p = add(h.p, off);
+}
+
+// y-rotation enter / cleanup (:1192-1237): the ray is rotated in place and back (ulp drift kept)
+__device__ __forceinline__ void rotate_enter(Trav &T, Ray &r, float sn, float cs) {
+  T.was_last = false;
+  const f3 o = r.o, d = r.d;
+  r.o = mk((cs * o.x) - (sn * o.z), o.y, (sn * o.x) + (cs * o.z));
+  r.d = mk((cs * d.x) - (sn * d.z), d.y, (sn * d.x) + (cs * d.z));
+  T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+}
+__device__ __forceinline__ void rotate_exit(Trav &T, Ray &r, Hit &h, float sn, float cs) {
+  const f3 o = r.o, d = r.d;
+  r.o = mk((cs * o.x) + (sn * o.z), o.y, (-sn * o.x) + (cs * o.z));
+  r.d = mk((cs * d.x) + (sn * d.z), d.y, (-sn * d.x) + (cs * d.z));
+  T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  if (T.was_last) {
+    const f3 p = h.p, n = h.n;
+    h.p = mk((cs * p.x) + (sn * p.z), p.y, (-sn * p.x) + (cs * p.z));
+    h.n = mk((cs * n.x) + (sn * n.z), n.y, (-sn * n.x) + (cs * n.z));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// traversal policy 1: per-lane DFS with a lane-interleaved LDS stack (any scene)
+// ---------------------------------------------------------------------------------------------
+// One iteration of hit()'s while loop (:1089-1249): pop one record and process it.
+template <bool LDS, bool COUNT, bool UV>
+__device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hit &h, uint16_t *stk, Visits &vc) {
+  int sp = T.sp - 1;
+  const uint32_t idx = stk[sp * 64];
+  const uint32_t nb = idx * kNodeWords;
+  const uint4 w0 = S.w4(nb);
+  const uint32_t kind = w0.x;
+  if (COUNT) { vc.k[kind < 7 ? kind : 0]++; }
+  const bool in_xf = T.tc || T.yc;
+  if (kind == K_BVH) {                                                     // :1124-1130
+    const uint4 w1 = S.w4(nb + 4);
+    if (box_hit(T, r, asf(w0.z), asf(w0.w), asf(w1.x), asf(w1.y), asf(w1.z), asf(w1.w))) {
+      stk[sp * 64] = static_cast<uint16_t>(w0.y >> 16);      // right
+      stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);      // left (popped first)
+      sp += 2;
+    }
+  } else if (kind == K_QUAD || kind == K_TRIANGLE) {
+    const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8), w3 = S.w4(nb + 12), w4 = S.w4(nb + 16);
+    planar_hit(T, r, h, kind == K_TRIANGLE, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), asf(w1.y),
+               mk(asf(w1.z), asf(w1.w), asf(w2.x)), mk(asf(w2.y), asf(w2.z), asf(w2.w)),
+               mk(asf(w3.x), asf(w3.y), asf(w3.z)), mk(asf(w3.w), asf(w4.x), asf(w4.y)), in_xf);
+  } else if (kind == K_SPHERE) {
+    const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8);
+    sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
+                   asf(w2.y), asf(w2.z), in_xf);
+  } else if (kind == K_TRANSLATE) {
+    const uint4 w1 = S.w4(nb + 4);
+    const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
+    if (T.tc == 0) {
+      translate_enter(T, r, off);
+      stk[sp * 64] = static_cast<uint16_t>(idx);
+      stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+      sp += 2;
+      T.tc++;
+    } else {
+      T.tc--;
+      translate_exit(T, r, h, off);
+    }
+  } else if (kind == K_YROTATE) {
+    if (T.yc == 0) {
+      rotate_enter(T, r, asf(w0.z), asf(w0.w));
+      stk[sp * 64] = static_cast<uint16_t>(idx);
+      stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+      sp += 2;
+      T.yc++;
+    } else {
+      T.yc--;
+      rotate_exit(T, r, h, asf(w0.z), asf(w0.w));
+    }
+  } else if (kind == K_GROUP) {                                           // :1238-1247
+    const uint32_t first = w0.y, n = w0.z;
+    for (uint32_t i = 0; i < n; ++i) stk[(sp + i) * 64] = static_cast<uint16_t>(first + i);
+    sp += n;
+  }
+  if (COUNT && static_cast<uint32_t>(sp) > vc.max_sp) vc.max_sp = sp;
+  T.sp = sp;
+}
+
+struct LaneTrace {
+  template <bool LDS, bool COUNT, bool UV>
+  __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t, uint32_t,
+                                             uint16_t *stk, Trav &T, Ray &r, Hit &h, Visits &vc) {
+    if (!busy) return;
+    trav_reset(T, r);
+    stk[0] = static_cast<uint16_t>(A.root);
+    T.sp = 1;
+    while (T.sp > 0) trav_step<LDS, COUNT, UV>(S, T, r, h, stk, vc);
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// traversal policy 2: one DFS per wave with per-entry lane masks
+// ---------------------------------------------------------------------------------------------
+// The reference's DFS order is fixed by the scene, not by the ray: a hit BVH node pushes right then
+// left (:1127-1128), a group pushes its children in index order (:1243-1245), a transform pushes
+// itself then its child (:1181-1182, :1207-1208).  So all rays of a wave can share ONE stack whose
+// entries carry the set of lanes that pushed them: restricted to lane L, the shared stack IS lane L's
+// own stack at every moment, and lane L processes exactly its own node sequence in its own order.
+// Each popped node is processed once for all its lanes; its kind and data are wave-uniform (scalar
+// loads, scalar branches) and the stack lives in three VGPRs used as 64-entry lane-indexed arrays.
+typedef const __attribute__((address_space(4))) uint32_t *cnode_ptr;
+
+struct WStack {          // wave-uniform stack: entry e lives in lane e of each register
+  uint32_t node, mlo, mhi;
+  int sp;
+};
+
+__device__ __forceinline__ void wpush(WStack &W, uint32_t lane, uint32_t node, uint64_t mask) {
+  const bool here = lane == static_cast<uint32_t>(W.sp);   // write entry sp into lane sp
+  W.node = here ? node : W.node;
+  W.mlo = here ? static_cast<uint32_t>(mask) : W.mlo;
+  W.mhi = here ? static_cast<uint32_t>(mask >> 32) : W.mhi;
+  W.sp++;
+}
+
+struct PacketTrace {
+  template <bool LDS, bool COUNT, bool UV>
+  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &A, bool, uint64_t lanes,
+                                             uint32_t lane, uint16_t *, Trav &T, Ray &r, Hit &h, Visits &vc) {
+    cnode_ptr nodes = (cnode_ptr)(reinterpret_cast<uintptr_t>(A.scene));
+    trav_reset(T, r);
+    WStack W{0, 0, 0, 0};
+    wpush(W, lane, A.root, lanes);
+    int depth_seen = 1;
+    while (W.sp > 0) {
+      W.sp--;
+      // readlane returns int: go through uint32_t so the low half is not sign-extended
+      const uint32_t node = static_cast<uint32_t>(__builtin_amdgcn_readlane(W.node, W.sp));
+      const uint32_t mlo = static_cast<uint32_t>(__builtin_amdgcn_readlane(W.mlo, W.sp));
+      const uint32_t mhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(W.mhi, W.sp));
+      const uint64_t mask = (static_cast<uint64_t>(mhi) << 32) | mlo;
+      const bool active = (mask >> lane) & 1ull;
+      const uint32_t nb = node * kNodeWords;
+      const uint32_t kind = nodes[nb + W_KIND];
+      const uint32_t aux = nodes[nb + W_AUX];
+      const bool in_xf = T.tc || T.yc;
+      if (COUNT && active) vc.k[kind < 7 ? kind : 0]++;
+      if (kind == K_BVH) {
+        const float x0 = asf(nodes[nb + 2]), x1 = asf(nodes[nb + 3]), y0 = asf(nodes[nb + 4]);
+        const float y1 = asf(nodes[nb + 5]), z0 = asf(nodes[nb + 6]), z1 = asf(nodes[nb + 7]);
+        bool hit = false;
+        if (active) hit = box_hit(T, r, x0, x1, y0, y1, z0, z1);
+        const uint64_t hm = __ballot(hit);
+        if (hm) {
+          wpush(W, lane, aux >> 16, hm);        // right
+          wpush(W, lane, aux & 0xffffu, hm);    // left (popped first)
+        }
+      } else if (kind == K_QUAD || kind == K_TRIANGLE) {
+        const f3 n = mk(asf(nodes[nb + W_NORMAL]), asf(nodes[nb + W_NORMAL + 1]), asf(nodes[nb + W_NORMAL + 2]));
+        const f3 q = mk(asf(nodes[nb + W_Q]), asf(nodes[nb + W_Q + 1]), asf(nodes[nb + W_Q + 2]));
+        const f3 uu = mk(asf(nodes[nb + W_U]), asf(nodes[nb + W_U + 1]), asf(nodes[nb + W_U + 2]));
+        const f3 vv = mk(asf(nodes[nb + W_V]), asf(nodes[nb + W_V + 1]), asf(nodes[nb + W_V + 2]));
+        const f3 ww = mk(asf(nodes[nb + W_W]), asf(nodes[nb + W_W + 1]), asf(nodes[nb + W_W + 2]));
+        const float dd = asf(nodes[nb + W_D]);
+        if (active) planar_hit(T, r, h, kind == K_TRIANGLE, aux, n, dd, q, uu, vv, ww, in_xf);
+      } else if (kind == K_SPHERE) {
+        const f3 c0 = mk(asf(nodes[nb + W_CENTER]), asf(nodes[nb + W_CENTER + 1]), asf(nodes[nb + W_CENTER + 2]));
+        const f3 mv = mk(asf(nodes[nb + W_MOTION]), asf(nodes[nb + W_MOTION + 1]), asf(nodes[nb + W_MOTION + 2]));
+        const float rad2 = asf(nodes[nb + W_RADIUS2]), inv_rad = asf(nodes[nb + W_INV_RADIUS]);
+        if (active) sphere_hit<UV>(T, r, h, aux, c0, mv, rad2, inv_rad, in_xf);
+      } else if (kind == K_TRANSLATE) {
+        const f3 off = mk(asf(nodes[nb + W_OFFSET]), asf(nodes[nb + W_OFFSET + 1]), asf(nodes[nb + W_OFFSET + 2]));
+        bool enter = false;
+        if (active) {
+          if (T.tc == 0) { enter = true; translate_enter(T, r, off); T.tc++; }
+          else { T.tc--; translate_exit(T, r, h, off); }
+        }
+        const uint64_t em = __ballot(enter);
+        if (em) { wpush(W, lane, node, em); wpush(W, lane, aux, em); }
+      } else if (kind == K_YROTATE) {
+        const float sn = asf(nodes[nb + W_SIN]), cs = asf(nodes[nb + W_COS]);
+        bool enter = false;
+        if (active) {
+          if (T.yc == 0) { enter = true; rotate_enter(T, r, sn, cs); T.yc++; }
+          else { T.yc--; rotate_exit(T, r, h, sn, cs); }
+        }
+        const uint64_t em = __ballot(enter);
+        if (em) { wpush(W, lane, node, em); wpush(W, lane, aux, em); }
+      } else if (kind == K_GROUP) {
+        const uint32_t n = nodes[nb + W_COUNT];
+        for (uint32_t i = 0; i < n; ++i) wpush(W, lane, (aux + i) & 0xffffu, mask);
+      }
+      if (COUNT && W.sp > depth_seen) depth_seen = W.sp;
+    }
+    if (COUNT && static_cast<uint32_t>(depth_seen) > vc.max_sp) vc.max_sp = depth_seen;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// the render body (cuda_calc + ray_color)
+// ---------------------------------------------------------------------------------------------
+// Each loop iteration is one "round": lanes without a pixel take the next pixels of their wave's
+// 8x8 tile (ballot + prefix count: active-path compaction), every lane with a pixel traces one path
+// segment (Trace policy), then shades it.  A lane whose path ended unwinds, accumulates and
+// immediately starts its next camera sample, so every lane traces every round.  A lane owns one pixel
+// and runs that pixel's samples strictly in order (one XORWOW stream per pixel), so scheduling never
+// changes what a lane computes.
+template <int F, class Trace>
+__device__ __forceinline__ void render_body(const RenderArgs &A) {
+  constexpr bool LDS = (F & kVarLds) != 0, COUNT = (F & kVarCount) != 0;
+  constexpr bool NOISE = (F & kVarNoise) != 0, UV = (F & kVarUv) != 0;
+  Mem<LDS> S{A.scene};
+  if (LDS) {
+    const uint32_t n4 = A.scene_words / 4;
+    const uint4 *src = reinterpret_cast<const uint4 *>(A.scene);
+    uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
+    for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
+    __syncthreads();
+  }
+  const uint32_t lane = __lane_id();
+  const uint32_t wave = threadIdx.x >> 6;
+  uint16_t *stk = reinterpret_cast<uint16_t *>(g_lds + A.stack_lds_word) + wave * A.stack_cap * 64 + lane;
+  const uint32_t gtid = blockIdx.x * kBlock + threadIdx.x;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
+
+  bool busy = false;                      // lane owns a pixel
+  int32_t pix = 0, sample = 0;
+  uint32_t depth = 0;
+  Rng rng{0, 0, 0, 0, 0, 0};
+  Ray ray;
+  ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
+  f3 sum = mk(0, 0, 0);
+  Trav T;
+  T.inv = mk(0, 0, 0); T.tmax = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = false; T.result = false;
+  Hit h;
+  h.u = 0; h.v = 0; h.t = 0; h.mat = 0; h.front = false; h.p = mk(0, 0, 0); h.n = mk(0, 0, 0);
+  Visits vc{};
+  uint32_t c_bounce = 0, c_shade = 0, c_perlin = 0, c_samples = 0;
+
+  uint32_t chunk_pos = 0, chunk_end = 0;   // wave-uniform: ids of the wave's current tile
+  bool exhausted = false;
+
+  auto camera_ray = [&]() {                                                 // :1561-1578
+    const int32_t lr = pix / A.width, j = pix - lr * A.width;
+    const int32_t i = A.row_offset + lr * A.row_stride;
+    const f3 pp = add(mk(A.p00[0], A.p00[1], A.p00[2]),
+                      add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
+                          scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
+    if (A.defocus_angle <= 0) {
+      ray.o = mk(A.center[0], A.center[1], A.center[2]);
+    } else {                                                                // :1459-1476
+      float x, y;
+      for (;;) {
+        y = rng.bound(-1.0f, 1.0f);    // Vec3(x(), y(), 0): y drawn first
+        x = rng.bound(-1.0f, 1.0f);
+        float l = sqrtf(x * x + y * y + 0.0f * 0.0f);
+        if (l * l < 1.0f) break;
+      }
+      f3 c = mk(A.center[0], A.center[1], A.center[2]);
+      f3 u = mk(A.dfu[0], A.dfu[1], A.dfu[2]), v = mk(A.dfv[0], A.dfv[1], A.dfv[2]);
+      ray.o = add(c, add(scale(x, u), scale(y, v)));
+    }
+    float xo = rng.uniform() - 0.5f;
+    float yo = rng.uniform() - 0.5f;
+    ray.d = sub(pp, ray.o);
+    ray.d = add(ray.d, scale(xo, mk(A.du[0], A.du[1], A.du[2])));
+    ray.d = add(ray.d, scale(yo, mk(A.dv[0], A.dv[1], A.dv[2])));
+    ray.time = rng.uniform();
+    depth = 0;
+  };
+
+  for (;;) {
+    // ---- lanes without a pixel take the next pixels of the wave's tile ----
+    bool need = !busy;
+    uint64_t m = __ballot(need);
+    while (m != 0 && !exhausted) {
+      if (chunk_pos >= chunk_end) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(A.work, static_cast<uint32_t>(kChunk));
+        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+        if (base >= A.n_ids) { exhausted = true; break; }
+        chunk_pos = base;
+        chunk_end = min(base + static_cast<uint32_t>(kChunk), A.n_ids);
+      }
+      const uint32_t avail = chunk_end - chunk_pos;
+      const uint32_t rank = __popcll(m & lt_mask);
+      if (need && rank < avail) {
+        // tile-major id -> (local row, column); ids past the shard edge are skipped
+        const uint32_t id = chunk_pos + rank, tile = id >> 6, k = id & 63u;
+        const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
+        const uint32_t lr = ty * 8 + (k >> 3), j = tx * 8 + (k & 7u);
+        if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
+          pix = static_cast<int32_t>(lr * A.width + j);
+          need = false;
+          busy = true;
+          const uint32_t n = A.n_pixels;
+          rng.d = A.rng[pix]; rng.x0 = A.rng[n + pix]; rng.x1 = A.rng[2 * n + pix];
+          rng.x2 = A.rng[3 * n + pix]; rng.x3 = A.rng[4 * n + pix]; rng.x4 = A.rng[5 * n + pix];
+          sum = mk(0, 0, 0);
+          sample = 0;
+          camera_ray();
+        }
+      }
+      chunk_pos += min(static_cast<uint32_t>(__popcll(m)), avail);
+      m = __ballot(need);
+    }
+    const uint64_t lanes = __ballot(busy);
+    if (lanes == 0) break;   // queue exhausted and every lane idle
+
+    // ---- trace one path segment per busy lane (hit(), :1340) ----
+    Trace::template run<LDS, COUNT, UV>(S, A, busy, lanes, lane, stk, T, ray, h, vc);
+    if (!busy) continue;
+
+    // ---- shade (ray_color loop body, :1340-1359) ----
+    bool done = false;
+    f3 res = mk(0, 0, 0);
+    if (T.result) {
+      if (COUNT) c_shade++;
+      const uint32_t mbase = A.off_mats + h.mat * kMatWords;
+      const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
+      const uint32_t mkind = m0.x;
+      f3 emit = mk(0, 0, 0);
+      if (mkind == MAT_DIFFUSE_LIGHT) emit = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
+      // cuda_material_scatter: random_test first, then the unit vector (z, y, x) (:497-502, vec3.h:152-161)
+      const float random_test = rng.uniform();
+      f3 ruv;
+      for (;;) {
+        float z = rng.bound(-1.0f, 1.0f);
+        float y = rng.bound(-1.0f, 1.0f);
+        float x = rng.bound(-1.0f, 1.0f);
+        f3 v = mk(x, y, z);
+        float len = length(v);
+        float len2 = len * len;
+        if (len2 > 0.0f && len2 <= 1.0f) { ruv = scale(1.0f / len, v); break; }
+      }
+      bool scattered = false;
+      f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
+      if (mkind == MAT_LAMBERTIAN) {                                        // :458-465
+        scattered = true;
+        dir = add(h.n, ruv);
+        const float eps = 1e-8f;
+        if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = h.n;
+        att = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
+      } else if (mkind == MAT_METAL) {                                      // :466-472
+        f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, h.n), h.n));
+        dir = add(unit(rd), scale(asf(m1.y), ruv));
+        att = mk(asf(m0.z), asf(m0.w), asf(m1.x));
+        scattered = dot(dir, h.n) > 0;
+      } else if (mkind == MAT_DIELECTRIC) {                                 // :473-487
+        att = mk(1.0f, 1.0f, 1.0f);
+        const float ior = asf(m1.z);
+        const float ri = h.front ? (1.0f / ior) : ior;
+        const f3 ud = unit(ray.d);
+        const float cos_t = fminf(dot(flip(ud), h.n), 1.0f);
+        const float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        bool reflect_it = ri * sin_t > 1.0f;
+        if (!reflect_it) {
+          float r0 = (1.0f - ri) / (1.0f + ri);
+          r0 = r0 * r0;
+          reflect_it = (r0 + (1.0f - r0) * rt_pow5f(1.0f - cos_t)) > random_test;
+        }
+        if (reflect_it) {
+          dir = sub(ud, scale(2.0f * dot(ud, h.n), h.n));
+        } else {                                                            // refract (:416-422)
+          float ct = fminf(dot(flip(ud), h.n), 1.0f);
+          f3 perp = scale(ri, add(ud, scale(ct, h.n)));
+          float pl = length(perp);
+          f3 par = scale(-sqrtf(fabsf(1.0f - pl * pl)), h.n);
+          dir = add(perp, par);
+        }
+        scattered = true;
+      }
+      if (scattered) {
+        // push attenuation (the emission pushed with it is always 0: only lights emit and lights
+        // never scatter, raytracing.cu:439-450 vs :457-488), so the unwind adds +0.0f per level
+        float *slot = A.rc + (static_cast<size_t>(depth) * 3) * A.threads + gtid;
+        slot[0] = att.x;
+        slot[A.threads] = att.y;
+        slot[2 * static_cast<size_t>(A.threads)] = att.z;
+        depth++;
+        if (COUNT) c_bounce++;
+        ray.o = h.p;
+        ray.d = dir;
+        if (depth == mb) { done = true; res = mk(0, 0, 0); }           // max_bounces exhausted: black
+      } else {
+        done = true;
+        res = emit;
+      }
+    } else {
+      done = true;
+      res = mk(A.bg[0], A.bg[1], A.bg[2]);
+    }
+    if (done) {
+      for (int32_t k = static_cast<int32_t>(depth) - 1; k >= 0; --k) {      // :1362-1368
+        const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
+        res = mk(slot[0] * res.x + 0.0f, slot[A.threads] * res.y + 0.0f,
+                 slot[2 * static_cast<size_t>(A.threads)] * res.z + 0.0f);
+      }
+      sum = add(sum, res);
+      sample++;
+      if (COUNT) c_samples++;
+      if (sample == A.spp) {
+        float *o = A.out + 3 * static_cast<size_t>(pix);
+        o[0] = sum.x * A.sample_scale;
+        o[1] = sum.y * A.sample_scale;
+        o[2] = sum.z * A.sample_scale;
+        busy = false;
+      } else {
+        camera_ray();
+      }
+    }
+  }
+
+  if (COUNT) {
+    uint32_t vals[CNT_SLOTS] = {0};
+    for (int k = 0; k < 7; ++k) vals[k] = vc.k[k];
+    vals[CNT_BOUNCES] = c_bounce;
+    vals[CNT_SHADES] = c_shade;
+    vals[CNT_PERLIN] = c_perlin;
+    vals[CNT_SAMPLES] = c_samples;
+    for (int k = 0; k < CNT_SLOTS; ++k) {
+      if (k == CNT_MAX_STACK || k == CNT_OVERFLOW || k == CNT_RNG) continue;
+      unsigned long long v = vals[k];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0 && v) atomicAdd(&A.counters[k], v);
+    }
+    uint32_t ms = vc.max_sp;
+    for (int off = 32; off > 0; off >>= 1) ms = max(ms, static_cast<uint32_t>(__shfl_xor(ms, off)));
+    if (lane == 0) {
+      atomicMax(&A.counters[CNT_MAX_STACK], static_cast<unsigned long long>(ms));
+      if (ms > A.stack_cap) atomicAdd(&A.counters[CNT_OVERFLOW], 1ull);
+    }
+  }
+}
+
+}  // namespace rt

@@ -1,0 +1,100 @@
+// rt_layout.h — device-visible layout of the compiled scene and the kernel argument blocks.
+//
+// Shared by the host (scene_compile.cpp, rt_capi.cpp), the offline HIP kernels (rt_device.hip) and the
+// scene-specialised kernels compiled at run time with hipRTC (rt_jit.cpp), so it may only include
+// <stdint.h> (the one C header hipRTC provides).
+#pragma once
+#include <stdint.h>
+
+namespace rt {
+
+// node kinds == reference VisObject values (raytracing.cu:144-153)
+enum : uint32_t {
+  K_SPHERE = 0, K_BVH = 1, K_TRIANGLE = 2, K_QUAD = 3, K_TRANSLATE = 4, K_YROTATE = 5, K_GROUP = 6
+};
+
+// Every scene record becomes one 80-byte node (record indices preserved, WorldRefs resolved).
+// Word layout per kind (w0 = kind, w1 = aux):
+//   BVH      : w1 = left_href | right_href << 16, w2..w7 = x0 x1 y0 y1 z0 z1
+//   SPHERE   : w1 = material, w2..4 centre, w5..7 motion, w8 radius, w9 radius*radius, w10 1/radius
+//   TRI/QUAD : w1 = material, w2..4 normal, w5 d, w6..8 q, w9..11 u, w12..14 v, w15..17 w
+//   TRANSLATE: w1 = child, w2..4 offset
+//   YROTATE  : w1 = child, w2 sin, w3 cos
+//   GROUP    : w1 = first child, w2 = count
+constexpr int kNodeWords = 20;
+enum : int {
+  W_KIND = 0, W_AUX = 1,
+  W_BOX = 2,
+  W_CENTER = 2, W_MOTION = 5, W_RADIUS = 8, W_RADIUS2 = 9, W_INV_RADIUS = 10,
+  W_NORMAL = 2, W_D = 5, W_Q = 6, W_U = 9, W_V = 12, W_W = 15,
+  W_OFFSET = 2, W_SIN = 2, W_COS = 3, W_COUNT = 2,
+};
+
+// materials (raytracing.cu:78-99): 8 words; kinds == RTR_MAT_* (rt_ref_layout.h)
+constexpr int kMatWords = 8;
+enum : int { M_KIND = 0, M_TEX = 1, M_ALBEDO = 2, M_FUZZ = 5, M_IOR = 6 };
+enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
+
+// textures (raytracing.cu:38-54): 8 words
+constexpr int kTexWords = 8;
+enum : uint32_t { T_SOLID = 0, T_CHECKER = 1, T_IMAGE = 2, T_NOISE = 3 };
+enum : int {
+  T_KIND = 0,
+  T_RGB = 1,                                         // solid: w1..3
+  T_EVEN = 1, T_ODD = 2, T_INV_SCALE = 3,            // checker
+  T_PERLIN = 1, T_NOISE_SCALE = 3,                   // noise: perlin table index, scale
+  T_WIDTH = 1, T_HEIGHT = 2, T_PIXELS = 3, T_HAS_PIXELS = 4,   // image: pixel word offset into pool
+};
+
+// Perlin table: 256 gradients as float4 (xyz, pad) + 256 perm_x bytes (perm_y/z are never read,
+// perlin_noise.cpp:37-39)
+constexpr int kPerlinWords = 256 * 4 + 64;
+
+// counter slots == RT_CNT_* (rt_render.h)
+enum : int {
+  CNT_VISIT0 = 0, CNT_BOUNCES = 7, CNT_SHADES = 8, CNT_PERLIN = 9, CNT_RNG = 10, CNT_SAMPLES = 11,
+  CNT_MAX_STACK = 12, CNT_OVERFLOW = 13, CNT_SLOTS = 16
+};
+
+constexpr int kBlock = 256;        // 4 waves of 64
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kChunk = 64;         // pixel ids handed to a wave per work-queue grab (one 8x8 tile)
+
+// render-kernel variants: scene staged in LDS, counters, Perlin noise textures, sphere u,v (image
+// textures with pixels), wave-packet traversal.  Specialising keeps unused texture code out of the
+// register allocation (the Perlin + double-sine path alone costs ~40 VGPRs).
+enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket = 16 };
+
+struct RenderArgs {
+  const uint32_t *scene;      // compiled scene word image in HBM
+  uint32_t scene_words;
+  uint32_t off_mats, off_texs, off_perlin, off_pixels, pixel_words;
+  uint32_t root, stack_cap, stack_lds_word;   // per-lane stack region starts at this LDS word
+  // camera (rt_camera)
+  float p00[3], du[3], dv[3], center[3], dfu[3], dfv[3], defocus_angle;
+  int32_t width, row_offset, row_stride;
+  int32_t spp, max_bounces;
+  float bg[3];
+  float sample_scale;
+  uint32_t n_pixels;          // row_count * width (local pixels of this shard)
+  uint32_t rows;              // row_count
+  uint32_t tiles_x;           // ceil(width / 8)
+  uint32_t n_ids;             // 64 * ceil(rows/8) * tiles_x: tile-major pixel ids handed to waves
+  const uint32_t *rng;        // [6][n_pixels] seeded XORWOW states {d, x0..x4}
+  float *out;                 // [n_pixels][3]
+  float *rc;                  // attenuation stack: [max_bounces][3][threads]
+  uint32_t threads;           // grid size in threads (rc stride)
+  uint32_t *work;             // chunk counter (zeroed per launch)
+  unsigned long long *counters;   // CNT_SLOTS (counting variants only)
+};
+
+struct SeedArgs {
+  const uint32_t *jump;       // xorwow_jump_tables() on device
+  uint32_t base[6];           // rocRAND constant seeding of `seed`
+  int32_t width, row_offset, row_stride;
+  uint32_t n_pixels;
+  uint32_t per_thread;
+  uint32_t *rng;              // [6][n_pixels]
+};
+
+}  // namespace rt

@@ -8,11 +8,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "gpu_scene.h"
+#include "rt_jit.h"
 #include "rt_kernels.h"
 #include "rt_render.h"
 #include "xorwow_jump.h"
@@ -54,6 +57,13 @@ int params_check(const rt_params *p) {
 
 }  // namespace
 
+static_assert(rt::MAT_LAMBERTIAN == RTR_MAT_LAMBERTIAN && rt::MAT_METAL == RTR_MAT_METAL &&
+              rt::MAT_DIELECTRIC == RTR_MAT_DIELECTRIC && rt::MAT_DIFFUSE_LIGHT == RTR_MAT_DIFFUSE_LIGHT, "mat kinds");
+static_assert(rt::CNT_BOUNCES == RT_CNT_BOUNCES && rt::CNT_SHADES == RT_CNT_SHADES && rt::CNT_PERLIN == RT_CNT_PERLIN &&
+              rt::CNT_SAMPLES == RT_CNT_SAMPLES && rt::CNT_MAX_STACK == RT_CNT_MAX_STACK &&
+              rt::CNT_OVERFLOW == RT_CNT_STACK_OVERFLOW && rt::CNT_SLOTS == RT_CNT__COUNT, "counter slots");
+static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::K_GROUP == RTR_OBJ_GROUP, "kinds");
+
 struct rt_context {
   int device = 0;
   int cu_count = 0;
@@ -62,6 +72,13 @@ struct rt_context {
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   bool lds = false;
   bool counted = false;
+  int variant = 0;
+  // traversal policy: -1 auto, RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC (env RT_TRAVERSAL for A/B runs)
+  int traversal = -1;
+  int used_traversal = RT_TRAV_LANE;
+  uint32_t jit_budget = 256;    // max node visits of a scene-specialised traversal (env RT_JIT_BUDGET)
+  uint32_t jit_visits = 0;
+  std::string jit_why;
   bool rendered = false;
   uint64_t samples = 0;
   size_t lds_bytes = 0;
@@ -112,6 +129,8 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   rt_context *c = new (std::nothrow) rt_context();
   if (!c) return RT_ERR_INVALID_ARG;
   c->device = device;
+  if (const char *e = std::getenv("RT_TRAVERSAL")) c->traversal = std::atoi(e);
+  if (const char *e = std::getenv("RT_JIT_BUDGET")) c->jit_budget = static_cast<uint32_t>(std::atoi(e));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
@@ -162,7 +181,35 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   const uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
   const size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * c->img.stack_need * 64 * 2;
   c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + stack_bytes;
-  const int per_cu = rt::render_blocks_per_cu(c->lds, c->counted, c->lds_bytes);
+  c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
+               (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
+  // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
+  // at most jit_budget node visits (every catalog scene but the large random ones), else the per-lane
+  // DFS.  The wave-packet DFS is kept as an explicit option (fastest on tiny all-sphere scenes).
+  int trav = c->traversal;
+  if (p->flags & RT_FLAG_FORCE_LANE) trav = RT_TRAV_LANE;
+  else if (p->flags & RT_FLAG_FORCE_PACKET) trav = RT_TRAV_PACKET;
+  else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
+  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC)) trav = RT_TRAV_LANE;
+  if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
+  hipFunction_t jit_fn = nullptr;
+  if (trav < 0 || trav == RT_TRAV_STATIC) {
+    rt::JitKernels jk;
+    std::string why;
+    if (rt::jit_kernels(c->img, c->variant, c->jit_budget, &jk, &why)) {
+      jit_fn = c->counted ? jk.render_count : jk.render;
+      c->jit_visits = jk.visits;
+      trav = RT_TRAV_STATIC;
+    } else {
+      c->jit_why = why;
+      trav = RT_TRAV_LANE;
+    }
+  }
+  if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
+  if (jit_fn) c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4;   // straight-line traversal: no stacks
+  c->used_traversal = trav;
+  const int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes)
+                            : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
   uint64_t blocks = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(c->cu_count);
   const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
   blocks = std::max<uint64_t>(1, std::min(blocks, needed));
@@ -188,7 +235,6 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.root = c->img.root;
   a.stack_cap = c->img.stack_need;
   a.stack_lds_word = scene_lds_words;
-  a.needs_uv = c->img.needs_uv ? 1u : 0u;
   const rtr_vec3 *v3s[6] = {&cam->pixel00, &cam->delta_u, &cam->delta_v, &cam->center, &cam->defocus_u, &cam->defocus_v};
   float *dst[6] = {a.p00, a.du, a.dv, a.center, a.dfu, a.dfv};
   for (int k = 0; k < 6; ++k) { dst[k][0] = v3s[k]->x; dst[k][1] = v3s[k]->y; dst[k][2] = v3s[k]->z; }
@@ -199,6 +245,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.bg[0] = p->background.x; a.bg[1] = p->background.y; a.bg[2] = p->background.z;
   a.sample_scale = 1.0f / static_cast<float>(p->samples_per_pixel);   // :1657
   a.n_pixels = n;
+  a.rows = static_cast<uint32_t>(p->row_count);
+  a.tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
+  a.n_ids = 64u * ((a.rows + 7) / 8) * a.tiles_x;
   a.rng = static_cast<const uint32_t *>(c->rng.p);
   a.out = out_dev;
   a.rc = static_cast<float *>(c->rc.p);
@@ -211,8 +260,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   if (hipEventRecord(c->ev[0], s) != hipSuccess) return RT_ERR_HIP;
   if (rt::launch_seed(sa, s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[1], s) != hipSuccess) return RT_ERR_HIP;
-  if (rt::launch_render(a, c->lds, c->counted, static_cast<uint32_t>(blocks), c->lds_bytes, s) != hipSuccess)
-    return RT_ERR_HIP;
+  const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
+                               : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
+  if (le != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
   return RT_OK;
 }
@@ -222,6 +272,8 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   std::memset(st, 0, sizeof *st);
   st->stack_needed = static_cast<int32_t>(c->img.stack_need);
   st->scene_in_lds = c->lds ? 1 : 0;
+  st->traversal = c->used_traversal;
+  st->jit_visits = static_cast<int32_t>(c->jit_visits);
   if (!c->rendered) return RT_OK;
   DeviceGuard g(c->device);
   if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;
@@ -267,3 +319,44 @@ int rt_render(const rt_scene *scene, const rt_camera *cam, const rt_params *p, f
 }
 
 }  // extern "C"
+
+namespace {
+void copy_out(const std::string &s, char *buf, uint64_t cap) {
+  if (!buf || cap == 0) return;
+  const size_t n = std::min<size_t>(s.size(), static_cast<size_t>(cap - 1));
+  std::memcpy(buf, s.data(), n);
+  buf[n] = '\0';
+}
+}  // namespace
+
+int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint64_t cap, uint32_t *visits) {
+  if (!scene) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  const int rc = rt::compile_scene(scene, &img);
+  if (rc != RT_OK) return rc;
+  std::string src;
+  uint32_t v = 0;
+  const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0);
+  const bool ok = rt::jit_source(img, variant, max_visits, &src, &v);
+  if (visits) *visits = v;
+  if (!ok) return RT_ERR_UNSUPPORTED;
+  copy_out(src, buf, cap);
+  return RT_OK;
+}
+
+int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *arch, char *log, uint64_t cap) {
+  if (!scene || !arch) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  const int rc = rt::compile_scene(scene, &img);
+  if (rc != RT_OK) return rc;
+  std::string src, lg;
+  uint32_t v = 0;
+  const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0);
+  if (!rt::jit_source(img, variant, max_visits, &src, &v)) return RT_ERR_UNSUPPORTED;
+  std::vector<char> code;
+  const bool ok = rt::jit_compile(src, arch, &code, &lg);
+  copy_out(lg, log, cap);
+  return ok ? RT_OK : RT_ERR_HIP;
+}
+
+const char *rt_context_note(const rt_context *c) { return c ? c->jit_why.c_str() : ""; }

@@ -1,590 +1,24 @@
-// rt_device.hip — MI355X (gfx950) kernels for the per-pixel render path.
+// rt_device.hip — offline-compiled MI355X (gfx950) kernels: generic render variants + RNG seeding.
 //
-// Replaces cuda_calc (raytracing.cu:1543-1589) + ray_color (:1333-1371) + hit (:1079-1251) +
-// materials/textures/Perlin (:356-502, perlin_noise.cpp) and init_gpu_data's curand_init (:1591-1606).
-//
-// Design:
-//  * persistent waves pull 64-pixel chunks from one HBM counter; a lane whose pixel finished takes the
-//    next pixel of its wave's chunk by ballot + prefix count (mbcnt), so lanes never idle on a
-//    finished pixel while the queue has work (active-path compaction across samples and pixels);
-//  * path regeneration: each loop iteration traces one segment per lane; a lane whose path ended
-//    unwinds its colour stack, accumulates and starts its next camera sample in the same iteration;
-//  * scene image (nodes / materials / textures / Perlin tables) staged in LDS when <= 48 KiB, else read
-//    through L1/L2 (read-only); traversal stack in LDS, lane-interleaved (conflict-free u16 slots);
-//  * per-pixel sums stay in registers (the reference read-modify-writes HBM every sample); only the
-//    attenuation stack spills to a coalesced [bounce][channel][thread] scratch buffer;
-//  * arithmetic is the reference's, op for op: compiled with -ffp-contract=off and correctly rounded
-//    f32 divide/sqrt, ternary MIN/MAX semantics, same draw order — bit-exact vs the oracle.
+// The render body lives in device/rt_body.h (shared with the scene-specialised kernels that rt_jit.cpp
+// compiles at run time).  Here it is instantiated with the two scene-independent traversal policies:
+//   LaneTrace   per-lane DFS over a lane-interleaved LDS stack (any scene size)
+//   PacketTrace one DFS per wave with per-entry lane masks (scalar node loads, uniform branches)
+// and the variant bits of rt_layout.h (LDS staging, counters, noise textures, image u,v).
 #include <hip/hip_runtime.h>
-#include <cstdint>
 
-#include "gpu_scene.h"
+#include "device/rt_body.h"
 #include "rt_kernels.h"
-#include "rt_render.h"
 
 namespace rt {
-namespace {
 
-extern __shared__ uint32_t g_lds[];   // [scene image (LDS variant)] [traversal stacks]
-
-struct f3 { float x, y, z; };
-__device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
-__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ f3 scale(float s, f3 v) { return mk(v.x * s, v.y * s, v.z * s); }
-__device__ __forceinline__ f3 flip(f3 v) { return mk(-v.x, -v.y, -v.z); }
-__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ f3 cross(f3 a, f3 b) {
-  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
-}
-__device__ __forceinline__ float length(f3 v) { return sqrtf(v.x * v.x + v.y * v.y + v.z * v.z); }
-__device__ __forceinline__ f3 unit(f3 v) {              // vec3.h:106-114 (three divisions)
-  float l = length(v);
-  if (l == 0.0f) return mk(0.0f, 0.0f, 0.0f);
-  return mk(v.x / l, v.y / l, v.z / l);
-}
-__device__ __forceinline__ f3 line_at(f3 o, float t, f3 d) { return add(o, scale(t, d)); }
-__device__ __forceinline__ float tmin_(float a, float b) { return (a < b) ? a : b; }   // utility.h:6
-__device__ __forceinline__ float tmax_(float a, float b) { return (a < b) ? b : a; }   // utility.h:7
-__device__ __forceinline__ float asf(uint32_t u) { return __uint_as_float(u); }
-
-// |denom| >= 1e-8 (a double literal, raytracing.cu:1064) <=> |denom| >= the smallest float >= 1e-8
-constexpr float kDenomEps = 1.00000008274037099e-08f;   // 0x322BCC78
-static_assert(kDenomEps > 1e-8 && (kDenomEps - 1e-8) < 1e-15, "denominator threshold");
-
-// ---------------------------------------------------------------------------------------------
-// scene memory: one word image, either in LDS or in HBM (read-only)
-// ---------------------------------------------------------------------------------------------
-template <bool LDS>
-struct Mem {
-  const uint32_t *__restrict__ g;
-  __device__ __forceinline__ uint32_t w(uint32_t i) const { return LDS ? g_lds[i] : g[i]; }
-  __device__ __forceinline__ float f(uint32_t i) const { return asf(w(i)); }
-  __device__ __forceinline__ uint4 w4(uint32_t i) const {   // i % 4 == 0
-    return LDS ? *reinterpret_cast<const uint4 *>(&g_lds[i]) : *reinterpret_cast<const uint4 *>(&g[i]);
-  }
-  __device__ __forceinline__ uint32_t byte(uint32_t word_base, uint32_t b) const {
-    return LDS ? reinterpret_cast<const uint8_t *>(&g_lds[word_base])[b]
-               : reinterpret_cast<const uint8_t *>(&g[word_base])[b];
-  }
-};
-
-// ---------------------------------------------------------------------------------------------
-// RNG: rocRAND XORWOW (replaces cuRAND)
-// ---------------------------------------------------------------------------------------------
-struct Rng {
-  uint32_t d, x0, x1, x2, x3, x4;
-  __device__ __forceinline__ uint32_t next() {
-    uint32_t t = x0 ^ (x0 >> 2);
-    x0 = x1; x1 = x2; x2 = x3; x3 = x4;
-    x4 = (x4 ^ (x4 << 4)) ^ (t ^ (t << 1));
-    d += 362437u;
-    return d + x4;
-  }
-  __device__ __forceinline__ float uniform() {       // rocrand_uniform: (0, 1]
-    const float inv = 2.3283064e-10f;
-    return inv + (static_cast<float>(next()) * inv);
-  }
-  __device__ __forceinline__ float bound(float lo, float hi) { return lo + (hi - lo) * uniform(); }
-};
-
-// sinf substitute (identical algorithm in the oracle: float rounding of a double sine)
-__device__ __forceinline__ float rt_sinf(float xf) {
-  double x = static_cast<double>(xf);
-  if (!(fabs(x) < 1.0e6)) return static_cast<float>(sin(x));
-  const double two_over_pi = 6.36619772367581382433e-01;
-  const double p1 = 1.57079632673412561417e+00;
-  const double p2 = 6.07710050630396597660e-11;
-  const double p3 = 2.02226624871116645580e-21;
-  double k = floor(x * two_over_pi + 0.5);
-  double r = ((x - k * p1) - k * p2) - k * p3;
-  long q = static_cast<long>(k) & 3;
-  double r2 = r * r;
-  double s = r + r * r2 * (-1.66666666666666666667e-01 + r2 * (8.33333333333333333333e-03 +
-             r2 * (-1.98412698412698412698e-04 + r2 * (2.75573192239858906526e-06 +
-             r2 * (-2.50521083854417187751e-08 + r2 * (1.60590438368216145994e-10 +
-             r2 * (-7.64716373181981647590e-13 + r2 * 2.81145725434552076320e-15)))))));
-  double c = 1.0 + r2 * (-0.5 + r2 * (4.16666666666666666667e-02 + r2 * (-1.38888888888888888889e-03 +
-             r2 * (2.48015873015873015873e-05 + r2 * (-2.75573192239858906526e-07 +
-             r2 * (2.08767569878680989792e-09 + r2 * (-1.14707455977297247139e-11 +
-             r2 * 4.77947733238738529744e-14)))))));
-  double res = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-  return static_cast<float>(res);
-}
-
-__device__ __forceinline__ float rt_pow5f(float xf) {   // powf(x, 5.0f) substitute
-  double x = static_cast<double>(xf);
-  double x2 = x * x;
-  double x4 = x2 * x2;
-  return static_cast<float>(x4 * x);
-}
-
-// ---------------------------------------------------------------------------------------------
-// textures + Perlin (raytracing.cu:343-398, perlin_noise.cpp:1-46,72-85)
-// ---------------------------------------------------------------------------------------------
-template <bool LDS>
-__device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
-  float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
-  float u = p.x - fx, v = p.y - fy, w = p.z - fz;
-  int32_t i = static_cast<int32_t>(fx), j = static_cast<int32_t>(fy), k = static_cast<int32_t>(fz);
-  const uint32_t pb = tb + 1024;   // perm_x bytes
-  uint32_t pi0 = S.byte(pb, i & 255), pi1 = S.byte(pb, (i + 1) & 255);
-  uint32_t pj0 = S.byte(pb, j & 255), pj1 = S.byte(pb, (j + 1) & 255);
-  uint32_t pk0 = S.byte(pb, k & 255), pk1 = S.byte(pb, (k + 1) & 255);
-  float uu = u * u * (3 - 2 * u);
-  float vv = v * v * (3 - 2 * v);
-  float ww = w * w * (3 - 2 * w);
-  // (a*uu + (1-a)*(1-uu)) is exactly uu or 1-uu for every finite uu (and NaN either way)
-  float wu[2] = {1 - uu, uu}, wv[2] = {1 - vv, vv}, wwk[2] = {1 - ww, ww};
-  float du[2] = {u, u - 1.0f}, dv[2] = {v, v - 1.0f}, dw[2] = {w, w - 1.0f};
-  uint32_t pi[2] = {pi0, pi1}, pj[2] = {pj0, pj1}, pk[2] = {pk0, pk1};
-  float accum = 0.0f;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        uint32_t g = (pi[a] ^ pj[b] ^ pk[c]) & 255;
-        uint4 gr = S.w4(tb + 4 * g);
-        f3 grad = mk(asf(gr.x), asf(gr.y), asf(gr.z));
-        accum += wu[a] * wv[b] * wwk[c] * dot(grad, mk(du[a], dv[b], dw[c]));
-      }
-  return accum;
-}
-
-template <bool LDS, bool COUNT>
-__device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti, float u, float v, f3 p,
-                            uint32_t &perlin_count) {
-  for (int guard = 0; guard < 64; ++guard) {
-    const uint32_t b = A.off_texs + ti * kTexWords;
-    uint4 t0 = S.w4(b);
-    switch (t0.x) {
-      case T_SOLID:
-        return mk(asf(t0.y), asf(t0.z), asf(t0.w));
-      case T_CHECKER: {
-        float inv = asf(t0.w);
-        int32_t x = static_cast<int32_t>(floorf(inv * p.x));
-        int32_t y = static_cast<int32_t>(floorf(inv * p.y));
-        int32_t z = static_cast<int32_t>(floorf(inv * p.z));
-        bool even = ((x + y + z) & 1) == 0;
-        ti = even ? t0.y : t0.z;
-      } break;
-      case T_IMAGE: {
-        uint4 t1 = S.w4(b + 4);
-        if (t1.x == 0) return mk(1, 0, 1);
-        int32_t wd = static_cast<int32_t>(t0.y), ht = static_cast<int32_t>(t0.z);
-        float cu = (u < 0) ? 0 : ((u > 1) ? 1 : u);
-        float cv = 1.0f - ((v < 0) ? 0 : ((v > 1) ? 1 : v));
-        int32_t x = static_cast<int32_t>(cu * wd), y = static_cast<int32_t>(cv * ht);
-        x = (x < 0) ? 0 : ((x > wd) ? wd : x);
-        y = (y < 0) ? 0 : ((y > ht) ? ht : y);
-        uint64_t wo = static_cast<uint64_t>(t0.w) + 3ull * (static_cast<uint64_t>(y) * wd + x);
-        if (wo + 3 > A.pixel_words) return mk(0, 0, 0);
-        uint32_t o = A.off_pixels + static_cast<uint32_t>(wo);
-        return mk(S.f(o), S.f(o + 1), S.f(o + 2));
-      }
-      case T_NOISE: {
-        if (COUNT) perlin_count++;
-        const uint32_t tb = A.off_perlin + t0.y * kPerlinWords;
-        float accum = 0.0f, weight = 1.0f;
-        f3 q = p;
-        for (int oct = 0; oct < 7; ++oct) {
-          accum += weight * perlin_noise(S, tb, q);
-          weight *= 0.5f;
-          q = mk(q.x * 2, q.y * 2, q.z * 2);
-        }
-        float turb = fabsf(accum);
-        float s = 1 + rt_sinf(asf(t0.w) * p.z + 10 * turb);
-        return mk(0.5f * s, 0.5f * s, 0.5f * s);
-      }
-      default:
-        return mk(0, 0, 0);
-    }
-  }
-  return mk(0, 0, 0);
-}
-
-// ---------------------------------------------------------------------------------------------
-// traversal (raytracing.cu:1079-1251) — identical visit order, in-place ray transforms
-// ---------------------------------------------------------------------------------------------
-struct Ray { f3 o, d; float time; };
-struct Hit { f3 p, n; float t, u, v; uint32_t mat; bool front; };
-
-struct Visits { uint32_t k[7]; uint32_t max_sp; };
-
-template <bool LDS, bool COUNT>
-__device__ bool trace(const Mem<LDS> &S, const RenderArgs &A, Ray &r, Hit &h, uint16_t *stk, Visits &vc) {
-  float tmin = 0.001f, tmax = __builtin_huge_valf();
-  f3 inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);   // 1/dir, refreshed when dir changes
-  int sp = 1;
-  stk[0] = static_cast<uint16_t>(A.root);
-  int tc = 0, yc = 0;
-  bool was_last = false, result = false;
-  while (sp > 0) {
-    --sp;
-    const uint32_t idx = stk[sp * 64];
-    const uint32_t nb = idx * kNodeWords;
-    const uint4 w0 = S.w4(nb);
-    const uint32_t kind = w0.x;
-    if (COUNT) { vc.k[kind < 7 ? kind : 0]++; }
-    if (kind == K_BVH) {                                                     // :1124-1130, :990-1025
-      const uint4 w1 = S.w4(nb + 4);
-      const float x0 = asf(w0.z), x1 = asf(w0.w), y0 = asf(w1.x), y1 = asf(w1.y), z0 = asf(w1.z), z1 = asf(w1.w);
-      float t0 = tmin, t1 = tmax;
-      float a = (x0 - r.o.x) * inv.x, c = (x1 - r.o.x) * inv.x;
-      if (inv.x < 0.0f && a > c) { float s = a; a = c; c = s; }
-      t0 = tmax_(t0, a); t1 = tmin_(t1, c);
-      bool miss = t1 <= t0;
-      a = (y0 - r.o.y) * inv.y; c = (y1 - r.o.y) * inv.y;
-      if (inv.y < 0.0f && a > c) { float s = a; a = c; c = s; }
-      t0 = tmax_(t0, a); t1 = tmin_(t1, c);
-      miss |= t1 <= t0;
-      a = (z0 - r.o.z) * inv.z; c = (z1 - r.o.z) * inv.z;
-      if (inv.z < 0.0f && a > c) { float s = a; a = c; c = s; }
-      t0 = tmax_(t0, a); t1 = tmin_(t1, c);
-      miss |= t1 <= t0;
-      if (!miss) {
-        stk[sp * 64] = static_cast<uint16_t>(w0.y >> 16);      // right
-        stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);      // left (popped first)
-        sp += 2;
-      }
-    } else if (kind == K_QUAD || kind == K_TRIANGLE) {                      // :1131-1175, :1060-1077
-      const uint4 w1 = S.w4(nb + 4);
-      const f3 n = mk(asf(w0.z), asf(w0.w), asf(w1.x));
-      const float dd = asf(w1.y);
-      float denom = dot(n, r.d);
-      if (fabsf(denom) >= kDenomEps) {
-        float t = (dd - dot(n, r.o)) / denom;
-        if (tmin <= t && t <= tmax) {
-          const uint4 w2 = S.w4(nb + 8), w3 = S.w4(nb + 12), w4 = S.w4(nb + 16);
-          const f3 q = mk(asf(w1.z), asf(w1.w), asf(w2.x));
-          const f3 uu = mk(asf(w2.y), asf(w2.z), asf(w2.w));
-          const f3 vv = mk(asf(w3.x), asf(w3.y), asf(w3.z));
-          const f3 ww = mk(asf(w3.w), asf(w4.x), asf(w4.y));
-          f3 p = line_at(r.o, t, r.d);
-          f3 pq = sub(p, q);
-          float alpha = dot(ww, cross(pq, vv));
-          float beta = dot(ww, cross(uu, pq));
-          bool inside = (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
-          if (kind == K_TRIANGLE) inside = inside && (alpha + beta <= 1.0f);
-          if (inside) {
-            h.u = alpha; h.v = beta; h.t = t; h.p = p; h.mat = w0.y;
-            h.front = dot(r.d, n) < 0;
-            h.n = h.front ? n : flip(n);
-            tmax = t;
-            result = true;
-            if (tc || yc) was_last = true;
-          }
-        }
-      }
-    } else if (kind == K_SPHERE) {                                          // :1093-1123
-      const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8);
-      const f3 c0 = mk(asf(w0.z), asf(w0.w), asf(w1.x));
-      const f3 mv = mk(asf(w1.y), asf(w1.z), asf(w1.w));
-      const float rad2 = asf(w2.y), inv_rad = asf(w2.z);
-      f3 center = line_at(c0, r.time, mv);
-      f3 oc = sub(center, r.o);
-      float a = dot(r.d, r.d);
-      float b = -2.0f * dot(r.d, oc);
-      float c = dot(oc, oc) - rad2;
-      float disc = b * b - 4 * a * c;
-      if (disc >= 0) {
-        float sq = sqrtf(disc);
-        float root = (-b - sq) / (2.0f * a);
-        if (tmin >= root || root >= tmax) root = (-b + sq) / (2.0f * a);
-        if (tmin < root && root < tmax) {
-          h.t = root;
-          h.p = line_at(r.o, root, r.d);
-          h.mat = w0.y;
-          f3 outward = scale(inv_rad, sub(h.p, center));
-          if (A.needs_uv) {                                                 // :583-590 (image textures only)
-            const float pi = 3.1415926535897932385f;
-            float theta = acosf(-outward.y);
-            float phi = atan2f(-outward.z, outward.x) + pi;
-            h.u = phi / (2 * pi);
-            h.v = theta / pi;
-          }
-          h.front = dot(r.d, outward) < 0;
-          h.n = h.front ? outward : flip(outward);
-          tmax = h.t;
-          result = true;
-          if (tc || yc) was_last = true;
-        }
-      }
-    } else if (kind == K_TRANSLATE) {                                       // :1176-1191
-      const uint4 w1 = S.w4(nb + 4);
-      const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
-      if (tc == 0) {
-        was_last = false;
-        r.o = sub(r.o, off);
-        stk[sp * 64] = static_cast<uint16_t>(idx);
-        stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
-        sp += 2;
-        tc++;
-      } else {
-        r.o = add(r.o, off);
-        tc--;
-        if (was_last) h.p = add(h.p, off);
-      }
-    } else if (kind == K_YROTATE) {                                         // :1192-1237
-      const float sn = asf(w0.z), cs = asf(w0.w);
-      const f3 o = r.o, d = r.d;
-      if (yc == 0) {
-        was_last = false;
-        r.o = mk((cs * o.x) - (sn * o.z), o.y, (sn * o.x) + (cs * o.z));
-        r.d = mk((cs * d.x) - (sn * d.z), d.y, (sn * d.x) + (cs * d.z));
-        stk[sp * 64] = static_cast<uint16_t>(idx);
-        stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
-        sp += 2;
-        yc++;
-      } else {
-        r.o = mk((cs * o.x) + (sn * o.z), o.y, (-sn * o.x) + (cs * o.z));
-        r.d = mk((cs * d.x) + (sn * d.z), d.y, (-sn * d.x) + (cs * d.z));
-        yc--;
-        if (was_last) {
-          const f3 p = h.p, n = h.n;
-          h.p = mk((cs * p.x) + (sn * p.z), p.y, (-sn * p.x) + (cs * p.z));
-          h.n = mk((cs * n.x) + (sn * n.z), n.y, (-sn * n.x) + (cs * n.z));
-        }
-      }
-      inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    } else if (kind == K_GROUP) {                                           // :1238-1247
-      const uint32_t first = w0.y, n = w0.z;
-      for (uint32_t i = 0; i < n; ++i) stk[(sp + i) * 64] = static_cast<uint16_t>(first + i);
-      sp += n;
-    }
-    if (COUNT && static_cast<uint32_t>(sp) > vc.max_sp) vc.max_sp = sp;
-  }
-  return result;
-}
-
-// ---------------------------------------------------------------------------------------------
-// the render kernel (cuda_calc + ray_color)
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-
-template <bool LDS, bool COUNT>
+template <int F>
 __global__ __launch_bounds__(kBlock) void render_kernel(RenderArgs A) {
-  Mem<LDS> S{A.scene};
-  if (LDS) {
-    const uint32_t n4 = A.scene_words / 4;
-    const uint4 *src = reinterpret_cast<const uint4 *>(A.scene);
-    uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
-    for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
-    __syncthreads();
-  }
-  const uint32_t lane = lane_id();
-  const uint32_t wave = threadIdx.x >> 6;
-  uint16_t *stk = reinterpret_cast<uint16_t *>(g_lds + A.stack_lds_word) + wave * A.stack_cap * 64 + lane;
-  const uint32_t gtid = blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
-
-  // lane state
-  int32_t pix = -1, sample = 0;
-  Rng rng{0, 0, 0, 0, 0, 0};
-  Ray ray;
-  ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
-  f3 pp = mk(0, 0, 0), sum = mk(0, 0, 0);
-  uint32_t depth = 0, bounces_left = 0;
-  Visits vc{};
-  uint32_t c_bounce = 0, c_shade = 0, c_perlin = 0, c_samples = 0;
-
-  // wave state (uniform)
-  uint32_t chunk_pos = 0, chunk_end = 0;
-  bool exhausted = false;
-
-  auto camera_ray = [&]() {                                                 // :1570-1578
-    if (A.defocus_angle <= 0) {
-      ray.o = mk(A.center[0], A.center[1], A.center[2]);
-    } else {                                                                // :1459-1476
-      float x, y;
-      for (;;) {
-        y = rng.bound(-1.0f, 1.0f);    // Vec3(x(), y(), 0): y drawn first
-        x = rng.bound(-1.0f, 1.0f);
-        float l = sqrtf(x * x + y * y + 0.0f * 0.0f);
-        if (l * l < 1.0f) break;
-      }
-      f3 c = mk(A.center[0], A.center[1], A.center[2]);
-      f3 u = mk(A.dfu[0], A.dfu[1], A.dfu[2]), v = mk(A.dfv[0], A.dfv[1], A.dfv[2]);
-      ray.o = add(c, add(scale(x, u), scale(y, v)));
-    }
-    float xo = rng.uniform() - 0.5f;
-    float yo = rng.uniform() - 0.5f;
-    ray.d = sub(pp, ray.o);
-    ray.d = add(ray.d, scale(xo, mk(A.du[0], A.du[1], A.du[2])));
-    ray.d = add(ray.d, scale(yo, mk(A.dv[0], A.dv[1], A.dv[2])));
-    ray.time = rng.uniform();
-    depth = 0;
-    bounces_left = mb;
-  };
-
-  for (;;) {
-    // ---- refill: lanes without a pixel take the next ones from the wave's chunk ----
-    bool need = pix < 0;
-    uint64_t m = __ballot(need);
-    while (m != 0 && !exhausted) {
-      if (chunk_pos >= chunk_end) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(A.work, static_cast<uint32_t>(kChunk));
-        base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
-        if (base >= A.n_pixels) { exhausted = true; break; }
-        chunk_pos = base;
-        chunk_end = min(base + static_cast<uint32_t>(kChunk), A.n_pixels);
-      }
-      const uint32_t avail = chunk_end - chunk_pos;
-      const uint32_t rank = __popcll(m & lt_mask);
-      if (need && rank < avail) {
-        pix = static_cast<int32_t>(chunk_pos + rank);
-        need = false;
-        const uint32_t n = A.n_pixels;
-        rng.d = A.rng[pix]; rng.x0 = A.rng[n + pix]; rng.x1 = A.rng[2 * n + pix];
-        rng.x2 = A.rng[3 * n + pix]; rng.x3 = A.rng[4 * n + pix]; rng.x4 = A.rng[5 * n + pix];
-        const int32_t lr = pix / A.width, j = pix - lr * A.width;
-        const int32_t i = A.row_offset + lr * A.row_stride;
-        pp = add(mk(A.p00[0], A.p00[1], A.p00[2]),
-                 add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
-                     scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
-        sum = mk(0, 0, 0);
-        sample = 0;
-        camera_ray();
-      }
-      const uint32_t took = min(static_cast<uint32_t>(__popcll(m)), avail);
-      chunk_pos += took;
-      m = __ballot(need);
-    }
-    if (__ballot(pix >= 0) == 0) break;
-    if (pix < 0) continue;
-
-    // ---- trace one path segment ----
-    Hit h;
-    h.u = 0; h.v = 0; h.t = 0; h.mat = 0; h.front = false; h.p = mk(0, 0, 0); h.n = mk(0, 0, 0);
-    const bool hit = trace<LDS, COUNT>(S, A, ray, h, stk, vc);
-
-    // ---- shade (ray_color loop body, :1340-1359) ----
-    bool done = false;
-    f3 res = mk(0, 0, 0);
-    if (hit) {
-      if (COUNT) c_shade++;
-      const uint32_t mbase = A.off_mats + h.mat * kMatWords;
-      const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
-      const uint32_t mkind = m0.x;
-      f3 emit = mk(0, 0, 0);
-      if (mkind == RTR_MAT_DIFFUSE_LIGHT) emit = texture_color<LDS, COUNT>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
-      // cuda_material_scatter: random_test first, then the unit vector (z, y, x) (:497-502, vec3.h:152-161)
-      const float random_test = rng.uniform();
-      f3 ruv;
-      for (;;) {
-        float z = rng.bound(-1.0f, 1.0f);
-        float y = rng.bound(-1.0f, 1.0f);
-        float x = rng.bound(-1.0f, 1.0f);
-        f3 v = mk(x, y, z);
-        float len = length(v);
-        float len2 = len * len;
-        if (len2 > 0.0f && len2 <= 1.0f) { ruv = scale(1.0f / len, v); break; }
-      }
-      bool scattered = false;
-      f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
-      if (mkind == RTR_MAT_LAMBERTIAN) {                                    // :458-465
-        scattered = true;
-        dir = add(h.n, ruv);
-        const float eps = 1e-8f;
-        if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = h.n;
-        att = texture_color<LDS, COUNT>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
-      } else if (mkind == RTR_MAT_METAL) {                                  // :466-472
-        f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, h.n), h.n));
-        dir = add(unit(rd), scale(asf(m1.y), ruv));
-        att = mk(asf(m0.z), asf(m0.w), asf(m1.x));
-        scattered = dot(dir, h.n) > 0;
-      } else if (mkind == RTR_MAT_DIELECTRIC) {                             // :473-487
-        att = mk(1.0f, 1.0f, 1.0f);
-        const float ior = asf(m1.z);
-        const float ri = h.front ? (1.0f / ior) : ior;
-        const f3 ud = unit(ray.d);
-        const float cos_t = fminf(dot(flip(ud), h.n), 1.0f);
-        const float sin_t = sqrtf(1.0f - cos_t * cos_t);
-        bool reflect_it = ri * sin_t > 1.0f;
-        if (!reflect_it) {
-          float r0 = (1.0f - ri) / (1.0f + ri);
-          r0 = r0 * r0;
-          reflect_it = (r0 + (1.0f - r0) * rt_pow5f(1.0f - cos_t)) > random_test;
-        }
-        if (reflect_it) {
-          dir = sub(ud, scale(2.0f * dot(ud, h.n), h.n));
-        } else {                                                            // refract (:416-422)
-          float ct = fminf(dot(flip(ud), h.n), 1.0f);
-          f3 perp = scale(ri, add(ud, scale(ct, h.n)));
-          float pl = length(perp);
-          f3 par = scale(-sqrtf(fabsf(1.0f - pl * pl)), h.n);
-          dir = add(perp, par);
-        }
-        scattered = true;
-      }
-      if (scattered) {
-        // push attenuation (emission pushed alongside is always 0: only lights emit and lights never
-        // scatter, raytracing.cu:439-450 vs :457-488), so the unwind adds +0.0f per level
-        float *slot = A.rc + (static_cast<size_t>(depth) * 3) * A.threads + gtid;
-        slot[0] = att.x;
-        slot[A.threads] = att.y;
-        slot[2 * static_cast<size_t>(A.threads)] = att.z;
-        depth++;
-        if (COUNT) c_bounce++;
-        ray.o = h.p;
-        ray.d = dir;
-        bounces_left--;
-        if (bounces_left == 0) { done = true; res = mk(0, 0, 0); }
-      } else {
-        done = true;
-        res = emit;
-      }
-    } else {
-      done = true;
-      res = mk(A.bg[0], A.bg[1], A.bg[2]);
-    }
-
-    if (done) {
-      for (int32_t k = static_cast<int32_t>(depth) - 1; k >= 0; --k) {    // :1362-1368
-        const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
-        res = mk(slot[0] * res.x + 0.0f, slot[A.threads] * res.y + 0.0f,
-                 slot[2 * static_cast<size_t>(A.threads)] * res.z + 0.0f);
-      }
-      sum = add(sum, res);
-      sample++;
-      if (COUNT) c_samples++;
-      if (sample == A.spp) {
-        float *o = A.out + 3 * static_cast<size_t>(pix);
-        o[0] = sum.x * A.sample_scale;
-        o[1] = sum.y * A.sample_scale;
-        o[2] = sum.z * A.sample_scale;
-        pix = -1;
-      } else {
-        camera_ray();
-      }
-    }
-  }
-
-  if (COUNT) {
-    uint32_t vals[RT_CNT__COUNT] = {0};
-    for (int k = 0; k < 7; ++k) vals[k] = vc.k[k];
-    vals[RT_CNT_BOUNCES] = c_bounce;
-    vals[RT_CNT_SHADES] = c_shade;
-    vals[RT_CNT_PERLIN] = c_perlin;
-    vals[RT_CNT_SAMPLES] = c_samples;
-    for (int k = 0; k < RT_CNT__COUNT; ++k) {
-      if (k == RT_CNT_MAX_STACK || k == RT_CNT_STACK_OVERFLOW || k == RT_CNT_RNG_DRAWS) continue;
-      unsigned long long v = vals[k];
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0 && v) atomicAdd(&A.counters[k], v);
-    }
-    uint32_t ms = vc.max_sp;
-    for (int off = 32; off > 0; off >>= 1) ms = max(ms, static_cast<uint32_t>(__shfl_xor(ms, off)));
-    if (lane == 0) {
-      atomicMax(&A.counters[RT_CNT_MAX_STACK], static_cast<unsigned long long>(ms));
-      if (ms > A.stack_cap) atomicAdd(&A.counters[RT_CNT_STACK_OVERFLOW], 1ull);
-    }
-  }
+  if constexpr ((F & kVarPacket) != 0) render_body<F, PacketTrace>(A);
+  else render_body<F, LaneTrace>(A);
 }
+
+namespace {
 
 // ---------------------------------------------------------------------------------------------
 // RNG seeding (init_gpu_data's curand_init, :1591-1606): state(i) = J^i * s0, i = global pixel
@@ -638,27 +72,25 @@ hipError_t launch_seed(const SeedArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <bool LDS, bool COUNT>
-static const void *kernel_ptr() { return reinterpret_cast<const void *>(&render_kernel<LDS, COUNT>); }
+template <int... Fs>
+struct KernelTable {
+  static constexpr int n = sizeof...(Fs);
+  const void *ptr[n] = {reinterpret_cast<const void *>(&render_kernel<Fs>)...};
+};
+static const KernelTable<0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+                         16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31> kKernels;
 
-hipError_t launch_render(const RenderArgs &a, bool lds, bool count, uint32_t blocks, size_t lds_bytes,
-                         hipStream_t s) {
-  dim3 g(blocks), b(kBlock);
-  if (lds) {
-    if (count) hipLaunchKernelGGL((render_kernel<true, true>), g, b, lds_bytes, s, a);
-    else hipLaunchKernelGGL((render_kernel<true, false>), g, b, lds_bytes, s, a);
-  } else {
-    if (count) hipLaunchKernelGGL((render_kernel<false, true>), g, b, lds_bytes, s, a);
-    else hipLaunchKernelGGL((render_kernel<false, false>), g, b, lds_bytes, s, a);
-  }
-  return hipGetLastError();
+hipError_t launch_render(const RenderArgs &a, int variant, uint32_t blocks, size_t lds_bytes, hipStream_t s) {
+  if (variant < 0 || variant >= kKernels.n) return hipErrorInvalidValue;
+  void *args[] = {const_cast<RenderArgs *>(&a)};
+  return hipLaunchKernel(kKernels.ptr[variant], dim3(blocks), dim3(kBlock), args, lds_bytes, s);
 }
 
-int render_blocks_per_cu(bool lds, bool count, size_t lds_bytes) {
-  const void *k = lds ? (count ? kernel_ptr<true, true>() : kernel_ptr<true, false>())
-                      : (count ? kernel_ptr<false, true>() : kernel_ptr<false, false>());
+int render_blocks_per_cu(int variant, size_t lds_bytes) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, lds_bytes) != hipSuccess || n <= 0) n = 1;
+  if (variant < 0 || variant >= kKernels.n ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kKernels.ptr[variant], kBlock, lds_bytes) != hipSuccess || n <= 0)
+    n = 1;
   return n;
 }
 

@@ -1,0 +1,132 @@
+// rt_jit.cpp — compile the scene-specialised render kernel (StaticTrace, scene_codegen.cpp) with hipRTC.
+//
+// The render body and the per-node helpers are the same source as the offline kernels
+// (device/rt_body.h, embedded here as text); only the traversal differs.  Compiled with the same
+// numerics flags as the offline build (-ffp-contract=off, correctly rounded f32 div/sqrt), so the
+// frames are bit-identical to the generic kernels'.  Modules are cached per (scene, variant, device).
+#include "rt_jit.h"
+
+#include <hip/hiprtc.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "device/embedded_headers.inc"
+
+namespace rt {
+namespace {
+
+struct Entry {
+  hipModule_t mod = nullptr;
+  JitKernels k;
+  bool ok = false;
+  std::string why;
+};
+
+std::mutex g_mu;
+std::map<std::string, std::unique_ptr<Entry>> g_cache;
+
+std::string arch_of(int dev) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return "gfx950";
+  std::string a = p.gcnArchName;
+  size_t c = a.find(':');
+  return c == std::string::npos ? a : a.substr(0, c);
+}
+
+}  // namespace
+
+bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::string *src, uint32_t *visits) {
+  std::string trace;
+  if (!generate_static_trace(img, max_visits, &trace, visits)) return false;
+  const int v = variant & (kVarLds | kVarNoise | kVarUv);
+  *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
+         "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render(RenderArgs A) {\n"
+         "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render_count(RenderArgs A) {\n"
+         "  render_body<" + std::to_string(v | kVarCount) + ", StaticTrace>(A);\n}\n"
+         "}  // namespace rt\n";
+  return true;
+}
+
+bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log) {
+  hiprtcProgram prog;
+  const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
+  const char *hdr_names[] = {"rt_layout.h", "rt_body.h"};
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_static.hip", 2, hdr_src, hdr_names) != HIPRTC_SUCCESS) {
+    if (log) *log = "hiprtcCreateProgram failed";
+    return false;
+  }
+  const std::string arch_opt = "--offload-arch=" + arch;
+  const char *opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                        "-fhip-fp32-correctly-rounded-divide-sqrt"};
+  const hiprtcResult r = hiprtcCompileProgram(prog, 6, opts);
+  bool ok = r == HIPRTC_SUCCESS;
+  if (log) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    log->assign(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &(*log)[0]);
+  }
+  if (ok) {
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code->resize(n);
+    ok = n > 0 && hiprtcGetCode(prog, code->data()) == HIPRTC_SUCCESS;
+  }
+  hiprtcDestroyProgram(&prog);
+  return ok;
+}
+
+bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKernels *out, std::string *why) {
+  std::string src;
+  uint32_t visits = 0;
+  if (!jit_source(img, variant, max_visits, &src, &visits)) {
+    if (why) *why = "scene expansion exceeds " + std::to_string(max_visits) + " node visits";
+    return false;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const std::string arch = arch_of(dev);
+  const std::string key = arch + "|" + std::to_string(dev) + "|" + src;
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_cache.find(key);
+  if (it == g_cache.end()) {
+    auto e = std::make_unique<Entry>();
+    std::vector<char> code;
+    std::string log;
+    if (!jit_compile(src, arch, &code, &log)) {
+      e->why = "hipRTC compile failed: " + log.substr(0, 2000);
+    } else if (hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
+               hipModuleGetFunction(&e->k.render, e->mod, "rt_static_render") != hipSuccess ||
+               hipModuleGetFunction(&e->k.render_count, e->mod, "rt_static_render_count") != hipSuccess) {
+      e->why = "hipModuleLoadData/GetFunction failed";
+    } else {
+      e->ok = true;
+      e->k.visits = visits;
+    }
+    it = g_cache.emplace(key, std::move(e)).first;
+  }
+  if (!it->second->ok) {
+    if (why) *why = it->second->why;
+    return false;
+  }
+  *out = it->second->k;
+  return true;
+}
+
+hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s) {
+  RenderArgs copy = a;
+  void *args[] = {&copy};
+  return hipModuleLaunchKernel(fn, blocks, 1, 1, kBlock, 1, 1, static_cast<unsigned>(lds_bytes), s, args, nullptr);
+}
+
+int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes) {
+  int n = 0;
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, lds_bytes) != hipSuccess || n <= 0) n = 1;
+  return n;
+}
+
+}  // namespace rt

@@ -1,0 +1,32 @@
+// rt_jit.h — scene-specialised render kernels compiled at run time with hipRTC.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "gpu_scene.h"
+
+namespace rt {
+
+struct JitKernels {
+  hipFunction_t render = nullptr;        // StaticTrace, no counters
+  hipFunction_t render_count = nullptr;  // StaticTrace, counters
+  uint32_t visits = 0;                   // node visits in the expanded traversal
+};
+
+// Compile (or fetch from the process-wide cache) the StaticTrace kernels of `img` for `variant`
+// (kVarLds | kVarNoise | kVarUv bits) on the current device.  Returns false (and a reason in *why)
+// when the scene is too large for the expansion budget or hipRTC is unavailable / fails: callers
+// then keep the generic kernels.
+bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKernels *out, std::string *why);
+
+// Full hipRTC source of the StaticTrace kernels for `variant` (no device needed).
+bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::string *src, uint32_t *visits);
+// Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
+bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
+
+hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s);
+int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes);
+
+}  // namespace rt

@@ -212,6 +212,40 @@ struct Compiler {
     return true;
   }
 
+  // No translation below a translation, no y-rotation below a y-rotation (see compile_scene).
+  bool transforms_well_nested(uint32_t root) {
+    // state per record: bit0 = reached under a translation, bit1 = under a rotation
+    std::vector<uint8_t> seen(sc->hittable_count, 0xff);
+    std::vector<std::pair<uint32_t, uint8_t>> work{{root, 0}};
+    while (!work.empty()) {
+      auto [i, ctx] = work.back();
+      work.pop_back();
+      if (seen[i] != 0xff && (seen[i] & ctx) == ctx) continue;
+      seen[i] = seen[i] == 0xff ? ctx : static_cast<uint8_t>(seen[i] | ctx);
+      const uint32_t *w = &nodes[static_cast<size_t>(i) * kNodeWords];
+      switch (w[W_KIND]) {
+        case K_BVH:
+          work.push_back({w[W_AUX] & 0xffff, ctx});
+          work.push_back({w[W_AUX] >> 16, ctx});
+          break;
+        case K_TRANSLATE:
+          if (ctx & 1) return false;
+          work.push_back({w[W_AUX], static_cast<uint8_t>(ctx | 1)});
+          break;
+        case K_YROTATE:
+          if (ctx & 2) return false;
+          work.push_back({w[W_AUX], static_cast<uint8_t>(ctx | 2)});
+          break;
+        case K_GROUP:
+          for (uint32_t k = 0; k < w[W_COUNT]; ++k) work.push_back({static_cast<uint16_t>(w[W_AUX] + k), ctx});
+          break;
+        default:
+          break;
+      }
+    }
+    return true;
+  }
+
   // Exact worst-case hit-stack depth of the DFS of raytracing.cu:1079-1251 starting at record i
   // (the record's own slot included).  -1 on a cycle / runaway depth.
   int32_t need(uint32_t i, int depth) {
@@ -268,6 +302,11 @@ int compile_scene(const void *scene_ptr, SceneImage *img) {
   c.need_memo.assign(sc->hittable_count, -1);
   int32_t need = c.need(root, 0);
   if (need < 0) return RT_ERR_SCENE;
+  // hit() keeps ONE translation and ONE y-rotation cleanup counter per ray (raytracing.cu:1084-1085):
+  // a translation reachable inside another translation's subtree (or a rotation inside a rotation)
+  // is taken for the outer one's cleanup marker and the outer one re-enters forever.  The reference
+  // hangs on such scenes; reject them instead of launching a kernel that never finishes.
+  if (!c.transforms_well_nested(root)) return RT_ERR_UNSUPPORTED;
 
   img->node_count = sc->hittable_count;
   img->mat_count = static_cast<uint32_t>(c.mats.size() / kMatWords);

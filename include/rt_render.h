@@ -77,6 +77,15 @@ typedef struct rt_params {
 
 #define RT_FLAG_COUNT       0x1u   /* collect traversal/shading counters into rt_stats.counters */
 #define RT_FLAG_GLOBAL_SCENE 0x2u  /* keep the scene in global memory even when it fits in LDS */
+#define RT_FLAG_NO_JIT      0x4u   /* never use the scene-specialised (hipRTC) traversal */
+#define RT_FLAG_FORCE_LANE   0x8u  /* force RT_TRAV_LANE   (A/B and parity tests; default: auto) */
+#define RT_FLAG_FORCE_PACKET 0x10u /* force RT_TRAV_PACKET (falls back to LANE if the stack is too deep) */
+#define RT_FLAG_FORCE_STATIC 0x20u /* force RT_TRAV_STATIC (falls back to LANE over the visit budget) */
+
+/* traversal policies (rt_stats.traversal) */
+#define RT_TRAV_LANE   0   /* per-lane DFS over an LDS stack (any scene) */
+#define RT_TRAV_PACKET 1   /* one DFS per wave with per-entry lane masks */
+#define RT_TRAV_STATIC 2   /* the scene's DFS expanded to straight-line code, compiled with hipRTC */
 
 /* rt_stats.counters[] slots (filled only with RT_FLAG_COUNT) */
 enum {
@@ -100,6 +109,8 @@ typedef struct rt_stats {
   uint64_t counters[RT_CNT__COUNT];
   int32_t stack_needed;    /* exact worst-case hit-stack depth of this scene */
   int32_t scene_in_lds;    /* 1 if the compiled scene was staged in LDS */
+  int32_t traversal;       /* RT_TRAV_* used by the last render */
+  int32_t jit_visits;      /* node visits of the specialised traversal (RT_TRAV_STATIC) */
 } rt_stats;
 
 /* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of
@@ -118,6 +129,15 @@ int rt_context_render(rt_context *ctx, const rt_camera *camera, const rt_params 
 /* Blocks on the last render's events; fills init/render ms, samples and (if counted) counters. */
 int rt_context_timing(rt_context *ctx, rt_stats *stats);
 void rt_context_destroy(rt_context *ctx);
+
+/* Diagnostics for the scene-specialised traversal (no device needed).
+ * rt_static_source: writes the hipRTC source for `scene` (NUL-terminated, truncated to cap) and the
+ *   number of node visits of the expanded DFS; RT_ERR_UNSUPPORTED if it exceeds max_visits.
+ * rt_static_compile: compiles that source for `arch` (e.g. "gfx950"); the compiler log goes to log. */
+int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint64_t cap, uint32_t *visits);
+int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *arch, char *log, uint64_t cap);
+/* Last fallback reason of a context (why RT_TRAV_STATIC was not used); "" if none. */
+const char *rt_context_note(const rt_context *ctx);
 
 const char *rt_status_string(int status);
 int rt_device_count(int *count);

@@ -172,3 +172,43 @@ def test_context_reuse_and_torch_buffers():
         ref, _ = gpu(w.scene(), cam, p)
         assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
     ctx.close()
+
+
+TRAVERSALS = [(rt.RT_FLAG_FORCE_LANE, rt.RT_TRAV_LANE), (rt.RT_FLAG_FORCE_PACKET, rt.RT_TRAV_PACKET),
+              (rt.RT_FLAG_FORCE_STATIC, rt.RT_TRAV_STATIC)]
+
+
+@pytest.mark.parametrize("idx", [0, 1, 8, 13, 15, 16, 17, 18, 19])
+def test_every_traversal_matches_oracle(idx):
+    # the three traversal policies (per-lane DFS, wave packet, hipRTC straight-line) must all reproduce
+    # the oracle bit for bit, with identical per-kind visit counts
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 40, 24)
+    p = rt.make_params(s, W, H, spp=3, bounces=min(s.max_bounces, 50), flags=rt.RT_FLAG_COUNT)
+    rc, ref, ost = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    for force, want in TRAVERSALS:
+        p.flags = rt.RT_FLAG_COUNT | force
+        fb, st = gpu(w.scene(), cam, p)
+        assert st.traversal == want, (force, st.traversal)
+        assert np.array_equal(bits(fb), bits(ref)), (idx, want)
+        g, o = st.counter_dict(), ost.counter_dict()
+        for k in ("visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate",
+                  "visit_yrotate", "visit_group", "bounces", "shades", "perlin", "samples"):
+            assert g[k] == o[k], (idx, want, k, g[k], o[k])
+
+
+def test_auto_policy_and_fallback():
+    # small scenes go through the specialised kernel, the 10k-sphere scene exceeds the visit budget
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 16, 9)
+    _, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4))
+    assert st.traversal == rt.RT_TRAV_STATIC and st.jit_visits > 0
+    _, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4, flags=rt.RT_FLAG_NO_JIT))
+    assert st.traversal != rt.RT_TRAV_STATIC
+    w, s = rt.build_scene(rt.RT_SCENE_RANDOM_10K)
+    cam, W, H = rt.camera_from_settings(s, 16, 9)
+    fb, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4, flags=rt.RT_FLAG_FORCE_STATIC))
+    assert st.traversal == rt.RT_TRAV_LANE
+    rc, ref, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4))
+    assert np.array_equal(bits(fb), bits(ref))

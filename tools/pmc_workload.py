@@ -1,0 +1,20 @@
+"""Profiling workload: one render of a bench configuration through the C-ABI (no torch needed)."""
+import argparse, sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import cuda_raytracing_amd as rt
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--scene", type=int, default=0)
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--spp", type=int, default=64)
+ap.add_argument("--bounces", type=int, default=16)
+ap.add_argument("--reps", type=int, default=1)
+a = ap.parse_args()
+w, s = rt.build_scene(a.scene)
+cam, W, H = rt.camera_from_settings(s, a.width, a.height)
+p = rt.make_params(s, W, H, spp=a.spp, bounces=a.bounces)
+for _ in range(a.reps):
+    fb, st = rt.render(w.scene(), cam, p, with_stats=True)
+print(f"render {st.render_ms:.3f} ms seed {st.init_ms:.3f} ms  {W*H*a.spp/st.render_ms/1e3:.1f} Msamples/s", flush=True)
