@@ -46,6 +46,9 @@ OPS_PER_SAMPLE_FIXED = 30                 # camera ray generation
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
+TRAV_NAMES = {0: "lane-dfs", 1: "wave-packet-dfs", 2: "scene-specialised"}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -55,16 +58,18 @@ def op_model(counters: dict, samples: int) -> float:
     return ops / max(samples, 1)
 
 
-def cpu_baseline(world, settings, W, H, spp, bounces, budget_s):
-    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample."""
+def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
+    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample.
+
+    The same sample is then rendered on the GPU through the product context and compared bit for bit
+    (the PSNR half of the BASELINE metric: identical frames -> PSNR = inf, reported as "bit-exact")."""
     import ctypes as C
     import numpy as np
     L = _abi.oracle_lib()
     cam, W, H = rt.camera_from_settings(settings, W, H)
-    stride = 8
-    rows = len(range(0, H, stride))
 
-    def run(s):
+    def run(stride, s):
+        rows = len(range(0, H, stride))
         p = rt.make_params(settings, W, H, spp=s, bounces=bounces, row_offset=0, row_stride=stride, row_count=rows)
         out = np.zeros((rows, W, 3), np.float32)
         st = _abi.Stats()
@@ -73,15 +78,33 @@ def cpu_baseline(world, settings, W, H, spp, bounces, budget_s):
                              C.byref(st))
         dt = time.perf_counter() - t
         assert rc == 0, rc
-        return rows * W * s, dt
+        return rows * W * s, dt, out
 
-    n, dt = run(2)                                   # calibration
-    rate = n / dt
-    s = int(max(2, min(spp, budget_s * rate / (rows * W))))
-    n, dt = run(s)
+    # calibrate on a sparse row sample (twice: the first call also spins up the OpenMP pool), then
+    # render every stride-th row of the frame at the FULL spp so the per-pixel work equals the GPU's
+    run(64, min(spp, 8))
+    n, dt, _ = run(64, min(spp, 8))
+    full_s = W * H * spp / (n / dt)
+    stride = max(1, math.ceil(full_s / budget_s))
+    rows = len(range(0, H, stride))
+    s = spp
+    n, dt, ref = run(stride, s)
+    parity = None
+    if ctx is not None:
+        import torch
+        p = rt.make_params(settings, W, H, spp=s, bounces=bounces, row_offset=0, row_stride=stride, row_count=rows)
+        dev = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
+        ctx.render_into(cam, p, dev.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        ctx.timing()
+        g = dev.cpu().numpy()
+        mse = float(np.mean((np.clip(np.sqrt(g), 0, 1) - np.clip(np.sqrt(ref), 0, 1)) ** 2))
+        parity = {"bit_exact": bool(np.array_equal(g.view(np.uint32), ref.view(np.uint32))),
+                  "psnr_db": None if mse == 0 else round(10 * math.log10(1.0 / mse), 2),
+                  "note": "GPU vs oracle on this sample; psnr_db null = identical frames (PSNR infinite)"}
     return {
         "value": n / dt / 1e6, "unit": "Msamples/s", "cores": int(L.rt_oracle_threads()), "kind": "port",
-        "sample": f"scene rows 0::{stride} ({rows} rows x {W} px) at spp {s}, d{bounces}: {n:.3g} samples in {dt:.1f} s",
+        "sample": f"frame rows 0::{stride} ({rows} rows x {W} px) at spp {s}, d{bounces}: {n:.3g} samples in {dt:.1f} s",
+        "parity": parity,
     }
 
 
@@ -90,8 +113,8 @@ def load_traffic(workload: str):
     if not f.exists():
         return None
     try:
-        d = json.loads(f.read_text())
-        return d.get(workload)
+        d = json.loads(f.read_text()).get(workload)
+        return int(d["bytes"]) if d else None
     except Exception:
         return None
 
@@ -106,7 +129,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--bounces", type=int, default=16)
-    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of oracle wall time")
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle wall time (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -192,6 +215,8 @@ def main():
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "parallelism": f"rows interleaved x{world_size}" + (" + RCCL gather" if world_size > 1 else ""),
                 "pixels_per_gpu": rows * W,
+                "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
+                "kernel": "rt_static_render (hipRTC)" if cst.traversal == rt.RT_TRAV_STATIC else "render_kernel",
             },
             "kernel_ms": {"render_mean": round(mean_render_ms, 3), "seed_mean": round(sum(init_ms) / len(init_ms), 3)},
             "roofline": {
@@ -208,7 +233,8 @@ def main():
         }
         if world_size == 1 and not args.no_cpu_baseline:
             try:
-                line["cpu_baseline"] = cpu_baseline(world, settings, W, H, args.spp, args.bounces, args.cpu_budget)
+                line["cpu_baseline"] = cpu_baseline(world, settings, W, H, args.spp, args.bounces, args.cpu_budget,
+                                                    ctx)
             except Exception as e:  # the baseline must never hide the GPU number
                 line["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
