@@ -545,6 +545,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 
   uint32_t chunk_pos = 0, chunk_end = 0;   // wave-uniform: ids of the wave's current tile
   bool exhausted = false;
+  uint32_t tiles_taken = 0, rounds = 0;
+  uint32_t probe_tile = 0, probe_rounds = 0;
+  uint64_t ph_refill = 0, ph_trace = 0, ph_shade = 0, t_mark = 0;   // wave-trace phase clocks
+  uint64_t busy_lane_rounds = 0;
+  const uint64_t t_start = A.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0;
 
   auto camera_ray = [&]() {                                                 // :1561-1578
     const int32_t lr = pix / A.width, j = pix - lr * A.width;
@@ -576,6 +581,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   };
 
   for (;;) {
+    if (A.wave_trace) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      if (t_mark) ph_shade += t - t_mark;
+      t_mark = t;
+    }
     // ---- lanes without a pixel take the next pixels of the wave's tile ----
     bool need = !busy;
     uint64_t m = __ballot(need);
@@ -585,6 +595,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         if (lane == 0) base = atomicAdd(A.work, static_cast<uint32_t>(kChunk));
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         if (base >= A.n_ids) { exhausted = true; break; }
+        if (A.reverse_tiles) base = A.n_ids - kChunk - base;   // whole tiles: n_ids is a multiple of 64
+        tiles_taken++;
         chunk_pos = base;
         chunk_end = min(base + static_cast<uint32_t>(kChunk), A.n_ids);
       }
@@ -592,16 +604,35 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       const uint32_t rank = __popcll(m & lt_mask);
       if (need && rank < avail) {
         // tile-major id -> (local row, column); ids past the shard edge are skipped
-        const uint32_t id = chunk_pos + rank, tile = id >> 6, k = id & 63u;
+        const uint32_t id = chunk_pos + rank;
+        uint32_t tile, k;
+        if (A.probe_cost) {                 // probe: a fixed spread of kProbePerTile pixels per tile
+          tile = id / kProbePerTile;
+          const uint32_t q = id - tile * kProbePerTile;
+          k = ((q * 5u + 1u) & 7u) * 8u + ((q * 3u + 2u) & 7u);
+        } else {
+          tile = id >> 6;
+          k = id & 63u;
+          if (A.tile_order) tile = A.tile_order[tile];
+        }
         const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
         const uint32_t lr = ty * 8 + (k >> 3), j = tx * 8 + (k & 7u);
         if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
           pix = static_cast<int32_t>(lr * A.width + j);
           need = false;
           busy = true;
-          const uint32_t n = A.n_pixels;
-          rng.d = A.rng[pix]; rng.x0 = A.rng[n + pix]; rng.x1 = A.rng[2 * n + pix];
-          rng.x2 = A.rng[3 * n + pix]; rng.x3 = A.rng[4 * n + pix]; rng.x4 = A.rng[5 * n + pix];
+          if (A.probe_cost) {               // throwaway stream: the real ones are not consumed
+            probe_tile = tile;
+            probe_rounds = 0;
+            uint32_t hsh = static_cast<uint32_t>(pix) * 0x9E3779B9u + 0x7F4A7C15u;
+            hsh ^= hsh >> 16; hsh *= 0x85EBCA6Bu; hsh ^= hsh >> 13; hsh *= 0xC2B2AE35u; hsh ^= hsh >> 16;
+            rng.d = hsh; rng.x0 = hsh ^ 0x2c7f967fu; rng.x1 = hsh * 3u + 1u; rng.x2 = ~hsh;
+            rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
+          } else {
+            const uint32_t n = A.n_pixels;
+            rng.d = A.rng[pix]; rng.x0 = A.rng[n + pix]; rng.x1 = A.rng[2 * n + pix];
+            rng.x2 = A.rng[3 * n + pix]; rng.x3 = A.rng[4 * n + pix]; rng.x4 = A.rng[5 * n + pix];
+          }
           sum = mk(0, 0, 0);
           sample = 0;
           camera_ray();
@@ -612,10 +643,23 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     const uint64_t lanes = __ballot(busy);
     if (lanes == 0) break;   // queue exhausted and every lane idle
+    rounds++;
+    busy_lane_rounds += static_cast<uint64_t>(__popcll(lanes));
+    if (A.wave_trace) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph_refill += t - t_mark;
+      t_mark = t;
+    }
 
     // ---- trace one path segment per busy lane (hit(), :1340) ----
     Trace::template run<LDS, COUNT, UV>(S, A, busy, lanes, lane, stk, T, ray, h, vc);
+    if (A.wave_trace) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph_trace += t - t_mark;
+      t_mark = t;
+    }
     if (!busy) continue;
+    probe_rounds++;
 
     // ---- shade (ray_color loop body, :1340-1359) ----
     bool done = false;
@@ -705,7 +749,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       sum = add(sum, res);
       sample++;
       if (COUNT) c_samples++;
-      if (sample == A.spp) {
+      if (A.probe_cost) {
+        atomicAdd(A.probe_cost + probe_tile, probe_rounds);
+        busy = false;
+      } else if (sample == A.spp) {
         float *o = A.out + 3 * static_cast<size_t>(pix);
         o[0] = sum.x * A.sample_scale;
         o[1] = sum.y * A.sample_scale;
@@ -717,6 +764,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
   }
 
+  if (A.wave_trace && lane == 0) {
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));   // HW_REG_XCC_ID
+    unsigned long long *w = A.wave_trace + kWaveTraceWords * static_cast<size_t>(blockIdx.x * kWavesPerBlock + wave);
+    w[0] = t_start; w[1] = t_end; w[2] = tiles_taken; w[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
+    w[4] = rounds; w[5] = busy_lane_rounds;
+    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade;
+  }
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};
     for (int k = 0; k < 7; ++k) vals[k] = vc.k[k];

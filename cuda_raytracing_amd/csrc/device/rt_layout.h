@@ -65,6 +65,10 @@ constexpr int kChunk = 64;         // pixel ids handed to a wave per work-queue 
 // register allocation (the Perlin + double-sine path alone costs ~40 VGPRs).
 enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket = 16 };
 
+// per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
+// refill / traversal / shading
+constexpr uint32_t kWaveTraceWords = 9;
+
 struct RenderArgs {
   const uint32_t *scene;      // compiled scene word image in HBM
   uint32_t scene_words;
@@ -86,7 +90,16 @@ struct RenderArgs {
   uint32_t threads;           // grid size in threads (rc stride)
   uint32_t *work;             // chunk counter (zeroed per launch)
   unsigned long long *counters;   // CNT_SLOTS (counting variants only)
+  unsigned long long *wave_trace; // diagnostics (null = off): kWaveTraceWords per wave
+  // Schedule.  A lane owns a pixel for all its samples (one XORWOW stream per pixel), so the frame
+  // ends when the slowest pixels end: tiles are handed out longest-first (LPT) using a cheap probe.
+  const uint32_t *tile_order;     // non-null: the t-th tile handed out is tile_order[t]
+  uint32_t *probe_cost;           // non-null: PROBE launch — kProbePerTile 1-spp paths per tile with
+                                  // a hashed RNG; adds each path's round count to probe_cost[tile]
+  uint32_t reverse_tiles;         // no order array: 1 = hand tiles out bottom row first
 };
+
+constexpr uint32_t kProbePerTile = 8;   // probe paths per 8x8 tile
 
 struct SeedArgs {
   const uint32_t *jump;       // xorwow_jump_tables() on device

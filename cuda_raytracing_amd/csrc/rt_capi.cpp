@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -64,11 +65,13 @@ static_assert(rt::CNT_BOUNCES == RT_CNT_BOUNCES && rt::CNT_SHADES == RT_CNT_SHAD
               rt::CNT_OVERFLOW == RT_CNT_STACK_OVERFLOW && rt::CNT_SLOTS == RT_CNT__COUNT, "counter slots");
 static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::K_GROUP == RTR_OBJ_GROUP, "kinds");
 
+constexpr int kLptMinSpp = 16;   // the probe costs 8 paths per 64-pixel tile: <1% of the frame from here
+
 struct rt_context {
   int device = 0;
   int cu_count = 0;
   SceneImage img;
-  DevBuf scene, jump, rng, rc, work, counters;
+  DevBuf scene, jump, rng, rc, work, counters, wave_trace, tile_cost, tile_order;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
   bool lds = false;
   bool counted = false;
@@ -79,6 +82,12 @@ struct rt_context {
   uint32_t jit_budget = 256;    // max node visits of a scene-specialised traversal (env RT_JIT_BUDGET)
   uint32_t jit_visits = 0;
   std::string jit_why;
+  // diagnostics / A-B knobs (env, read at creation): RT_WAVE_TRACE=<file>, RT_TILE_ORDER, RT_BLOCKS_PER_CU
+  std::string wave_trace_path;
+  size_t wave_trace_words = 0;
+  int sched = 0;   // RT_SCHED: 0 auto (longest-first when spp >= kLptMinSpp), 1 row-major, 2 reversed, 3 longest-first
+  int blocks_per_cu = 0;
+  bool used_lpt = false;
   bool rendered = false;
   uint64_t samples = 0;
   size_t lds_bytes = 0;
@@ -131,6 +140,9 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   c->device = device;
   if (const char *e = std::getenv("RT_TRAVERSAL")) c->traversal = std::atoi(e);
   if (const char *e = std::getenv("RT_JIT_BUDGET")) c->jit_budget = static_cast<uint32_t>(std::atoi(e));
+  if (const char *e = std::getenv("RT_WAVE_TRACE")) c->wave_trace_path = e;
+  if (const char *e = std::getenv("RT_SCHED")) c->sched = std::atoi(e);
+  if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
@@ -192,12 +204,13 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
   if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC)) trav = RT_TRAV_LANE;
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
-  hipFunction_t jit_fn = nullptr;
+  hipFunction_t jit_fn = nullptr, jit_plain = nullptr;
   if (trav < 0 || trav == RT_TRAV_STATIC) {
     rt::JitKernels jk;
     std::string why;
     if (rt::jit_kernels(c->img, c->variant, c->jit_budget, &jk, &why)) {
       jit_fn = c->counted ? jk.render_count : jk.render;
+      jit_plain = jk.render;
       c->jit_visits = jk.visits;
       trav = RT_TRAV_STATIC;
     } else {
@@ -210,7 +223,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   c->used_traversal = trav;
   const int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes)
                             : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
-  uint64_t blocks = static_cast<uint64_t>(per_cu) * static_cast<uint64_t>(c->cu_count);
+  uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
+                    static_cast<uint64_t>(c->cu_count);
   const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
   blocks = std::max<uint64_t>(1, std::min(blocks, needed));
   const uint32_t threads = static_cast<uint32_t>(blocks * rt::kBlock);
@@ -254,12 +268,48 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.threads = threads;
   a.work = static_cast<uint32_t *>(c->work.p);
   a.counters = static_cast<unsigned long long *>(c->counters.p);
+  a.tile_order = nullptr;
+  a.probe_cost = nullptr;
+  a.reverse_tiles = c->sched == 2 ? 1u : 0u;
+  const uint32_t n_tiles = a.n_ids / 64u;
+  c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
+  a.wave_trace = nullptr;
+  c->wave_trace_words = 0;
+  if (!c->wave_trace_path.empty()) {
+    c->wave_trace_words = static_cast<size_t>(blocks) * rt::kWavesPerBlock * rt::kWaveTraceWords;
+    if (c->wave_trace.ensure(c->wave_trace_words * 8) != hipSuccess) return RT_ERR_HIP;
+    if (hipMemsetAsync(c->wave_trace.p, 0, c->wave_trace_words * 8, s) != hipSuccess) return RT_ERR_HIP;
+    a.wave_trace = static_cast<unsigned long long *>(c->wave_trace.p);
+  }
 
   if (hipMemsetAsync(c->work.p, 0, 64, s) != hipSuccess) return RT_ERR_HIP;
   if (c->counted && hipMemsetAsync(c->counters.p, 0, RT_CNT__COUNT * 8, s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[0], s) != hipSuccess) return RT_ERR_HIP;
   if (rt::launch_seed(sa, s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[1], s) != hipSuccess) return RT_ERR_HIP;
+  if (c->used_lpt) {
+    // longest-first schedule: probe kProbePerTile throwaway 1-spp paths per tile (their own RNG,
+    // no output), then counting-sort tiles by probe cost; counted in render_ms
+    if (c->tile_cost.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess ||
+        c->tile_order.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
+      return RT_ERR_HIP;
+    if (hipMemsetAsync(c->tile_cost.p, 0, static_cast<size_t>(n_tiles) * 4, s) != hipSuccess) return RT_ERR_HIP;
+    rt::RenderArgs pa = a;
+    pa.probe_cost = static_cast<uint32_t *>(c->tile_cost.p);
+    pa.n_ids = n_tiles * rt::kProbePerTile;
+    pa.spp = 1;
+    pa.out = nullptr;
+    pa.rng = nullptr;
+    pa.work = static_cast<uint32_t *>(c->work.p) + 8;
+    pa.wave_trace = nullptr;
+    const hipError_t pe = jit_plain ? rt::jit_launch(jit_plain, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
+                                    : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
+                                                        c->lds_bytes, s);
+    if (pe != hipSuccess) return RT_ERR_HIP;
+    if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), s) != hipSuccess)
+      return RT_ERR_HIP;
+    a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
+  }
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
   if (le != hipSuccess) return RT_ERR_HIP;
@@ -287,6 +337,14 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
     unsigned long long h[RT_CNT__COUNT];
     if (hipMemcpy(h, c->counters.p, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
     for (int k = 0; k < RT_CNT__COUNT; ++k) st->counters[k] = h[k];
+  }
+  if (c->wave_trace_words) {   // diagnostics: raw per-wave records, appended per render
+    std::vector<unsigned long long> w(c->wave_trace_words);
+    if (hipMemcpy(w.data(), c->wave_trace.p, w.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
+    if (FILE *f = std::fopen(c->wave_trace_path.c_str(), "ab")) {
+      std::fwrite(w.data(), 8, w.size(), f);
+      std::fclose(f);
+    }
   }
   return RT_OK;
 }

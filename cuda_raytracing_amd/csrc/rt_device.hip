@@ -62,7 +62,42 @@ __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
   }
 }
 
+// Longest-first tile order from the probe costs: bucket by cost (1024 linear buckets of the max,
+// descending), counting sort in LDS.  One block; ~32k tiles at 1080p.  Order inside a bucket is
+// arbitrary — the schedule never changes what a lane computes.
+constexpr int kOrderThreads = 1024, kOrderBuckets = 1024;
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint32_t *cost, uint32_t n, uint32_t *order) {
+  __shared__ uint32_t hist[kOrderBuckets];
+  __shared__ uint32_t wmax[kOrderThreads / 64];
+  const uint32_t t = threadIdx.x;
+  uint32_t m = 0;
+  for (uint32_t i = t; i < n; i += kOrderThreads) m = max(m, cost[i]);
+  for (int off = 32; off > 0; off >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(m, off)));
+  if ((t & 63u) == 0) wmax[t >> 6] = m;
+  for (uint32_t b = t; b < kOrderBuckets; b += kOrderThreads) hist[b] = 0;
+  __syncthreads();
+  uint32_t mx = 1;
+  for (int w = 0; w < kOrderThreads / 64; ++w) mx = max(mx, wmax[w]);
+  auto key = [&](uint32_t c) {
+    const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(c) * (kOrderBuckets - 1)) / mx);
+    return static_cast<uint32_t>(kOrderBuckets - 1) - b;
+  };
+  for (uint32_t i = t; i < n; i += kOrderThreads) atomicAdd(&hist[key(cost[i])], 1u);
+  __syncthreads();
+  if (t == 0) {
+    uint32_t run = 0;
+    for (int b = 0; b < kOrderBuckets; ++b) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += kOrderThreads) order[atomicAdd(&hist[key(cost[i])], 1u)] = i;
+}
+
 }  // namespace
+
+hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s) {
+  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, s, cost, n, order);
+  return hipGetLastError();
+}
 
 hipError_t launch_seed(const SeedArgs &a, hipStream_t s) {
   const uint64_t threads = (static_cast<uint64_t>(a.n_pixels) + a.per_thread - 1) / a.per_thread;

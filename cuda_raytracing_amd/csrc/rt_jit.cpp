@@ -8,6 +8,9 @@
 
 #include <hip/hiprtc.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -77,6 +80,13 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
     ok = n > 0 && hiprtcGetCode(prog, code->data()) == HIPRTC_SUCCESS;
   }
   hiprtcDestroyProgram(&prog);
+  if (ok) {
+    if (const char *dir = std::getenv("RT_JIT_DUMP")) {   // diagnostics: source + code object
+      const std::string base = std::string(dir) + "/rt_static_" + std::to_string(std::hash<std::string>()(src));
+      if (FILE *f = std::fopen((base + ".hip").c_str(), "wb")) { std::fwrite(src.data(), 1, src.size(), f); std::fclose(f); }
+      if (FILE *f = std::fopen((base + ".co").c_str(), "wb")) { std::fwrite(code->data(), 1, code->size(), f); std::fclose(f); }
+    }
+  }
   return ok;
 }
 

@@ -212,3 +212,16 @@ def test_auto_policy_and_fallback():
     assert st.traversal == rt.RT_TRAV_LANE
     rc, ref, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4))
     assert np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("sched", ["0", "1", "2", "3"])
+def test_tile_schedules_agree(sched, monkeypatch):
+    # the schedule (longest-first probe order, row-major, reversed) only changes which lane renders a
+    # pixel when; frames must stay bit-identical to the oracle (spp >= 16 enables the probe in auto)
+    monkeypatch.setenv("RT_SCHED", sched)
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 37, 21)
+    p = rt.make_params(s, W, H, spp=16, bounces=8)
+    fb, _ = gpu(w.scene(), cam, p)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
