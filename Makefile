@@ -19,7 +19,7 @@ INC       := -Iinclude -I$(CSRC)
 # No FP contraction anywhere on the path: parity with the oracle is bit-exact.
 HOST_FLAGS := -O2 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wextra
 HIP_FLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
-              -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-rdc -Wall
+              -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-rdc -fno-slp-vectorize -Wall
 ORACLE_FLAGS := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -fopenmp -Wall -Wextra
 
 HOST_SRC := $(CSRC)/host/rt_host.cpp

@@ -82,9 +82,15 @@ def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
 
     # calibrate on a sparse row sample (twice: the first call also spins up the OpenMP pool), then
     # render every stride-th row of the frame at the FULL spp so the per-pixel work equals the GPU's
-    run(64, min(spp, 8))
-    n, dt, _ = run(64, min(spp, 8))
-    full_s = W * H * spp / (n / dt)
+    # calibrate: t = a*pixels (RNG seeding by jumps) + b*samples, from two short runs on every 16th row
+    run(16, 2)
+    s1, s2 = min(spp, 8), min(spp, 32)
+    n1, t1, _ = run(16, s1)
+    n2, t2, _ = run(16, s2)
+    px = n1 / s1
+    b = max((t2 - t1) / max(n2 - n1, 1), 1e-12) if s2 > s1 else t1 / n1
+    a = max((t1 - b * n1) / px, 0.0)
+    full_s = a * W * H + b * W * H * spp
     stride = max(1, math.ceil(full_s / budget_s))
     rows = len(range(0, H, stride))
     s = spp
@@ -176,11 +182,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    render_ms, init_ms = [], []
+    render_ms, init_ms, sched_ms = [], [], []
     for _ in range(args.steps):
         st = step()
         render_ms.append(st.render_ms)
         init_ms.append(st.init_ms)
+        sched_ms.append(st.sched_ms)
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -218,7 +225,8 @@ def main():
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
                 "kernel": "rt_static_render (hipRTC)" if cst.traversal == rt.RT_TRAV_STATIC else "render_kernel",
             },
-            "kernel_ms": {"render_mean": round(mean_render_ms, 3), "seed_mean": round(sum(init_ms) / len(init_ms), 3)},
+            "kernel_ms": {"render_mean": round(mean_render_ms, 3), "seed_mean": round(sum(init_ms) / len(init_ms), 3),
+                          "schedule_mean": round(sum(sched_ms) / len(sched_ms), 3)},
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved, 3),

@@ -90,6 +90,7 @@ class Stats(C.Structure):
         ("samples", C.c_uint64), ("counters", C.c_uint64 * 16),
         ("stack_needed", C.c_int32), ("scene_in_lds", C.c_int32),
         ("traversal", C.c_int32), ("jit_visits", C.c_int32),
+        ("sched_ms", C.c_double),
     ]
 
     def counter_dict(self):

@@ -13,7 +13,8 @@
 
 namespace rt {
 
-extern __shared__ uint32_t g_lds[];   // [scene image (LDS variant)] [per-lane traversal stacks]
+// [scene image (LDS variant)] [colour-stack levels 0..rc_lds_levels-1] [per-lane traversal stacks]
+extern __shared__ uint32_t g_lds[];
 
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -250,8 +251,10 @@ __device__ __forceinline__ void planar_hit(Trav &T, const Ray &r, Hit &h, bool t
       f3 pq = sub(p, q);
       float alpha = dot(ww, cross(pq, vv));
       float beta = dot(ww, cross(uu, pq));
-      bool inside = (0.0f <= alpha && alpha <= 1.0f) && (0.0f <= beta && beta <= 1.0f);
-      if (tri) inside = inside && (alpha + beta <= 1.0f);
+      // same predicate as (0 <= a && a <= 1) && (0 <= b && b <= 1) (NaN fails every compare), written
+      // with non-short-circuit ands so it stays four compares on the lane mask
+      bool inside = (0.0f <= alpha) & (alpha <= 1.0f) & (0.0f <= beta) & (beta <= 1.0f);
+      if (tri) inside = inside & (alpha + beta <= 1.0f);
       if (inside) {
         h.u = alpha; h.v = beta; h.t = t; h.p = p; h.mat = mat;
         h.front = dot(r.d, n) < 0;
@@ -525,6 +528,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const uint32_t lane = __lane_id();
   const uint32_t wave = threadIdx.x >> 6;
   uint16_t *stk = reinterpret_cast<uint16_t *>(g_lds + A.stack_lds_word) + wave * A.stack_cap * 64 + lane;
+  // colour stack: level k channel c at rc_l[(3k + c) * 64] (lane-interleaved, conflict-free) for
+  // k < rc_lds_levels, else in HBM at rc[(3k + c) * threads + gtid]
+  float *rc_l = reinterpret_cast<float *>(g_lds + A.rc_lds_word) + wave * A.rc_lds_levels * 192 + lane;
   const uint32_t gtid = blockIdx.x * kBlock + threadIdx.x;
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
@@ -606,10 +612,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         // tile-major id -> (local row, column); ids past the shard edge are skipped
         const uint32_t id = chunk_pos + rank;
         uint32_t tile, k;
-        if (A.probe_cost) {                 // probe: a fixed spread of kProbePerTile pixels per tile
-          tile = id / kProbePerTile;
-          const uint32_t q = id - tile * kProbePerTile;
-          k = ((q * 5u + 1u) & 7u) * 8u + ((q * 3u + 2u) & 7u);
+        if (A.probe_cost) {                 // probe: probe_per_tile distinct pixels spread over the tile
+          tile = id / A.probe_per_tile;
+          const uint32_t q = id - tile * A.probe_per_tile;
+          k = (q * 37u + 11u) & 63u;
         } else {
           tile = id >> 6;
           k = id & 63u;
@@ -678,11 +684,19 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         float z = rng.bound(-1.0f, 1.0f);
         float y = rng.bound(-1.0f, 1.0f);
         float x = rng.bound(-1.0f, 1.0f);
-        f3 v = mk(x, y, z);
-        float len = length(v);
-        float len2 = len * len;
-        if (len2 > 0.0f && len2 <= 1.0f) { ruv = scale(1.0f / len, v); break; }
+        // accept iff fl(fl(sqrt(s))^2) in (0, 1] (vec3.h:152-161, `1e-50 < len2` == `len2 > 0`).
+        // Decided on s itself except within 2^-20 of 1: s in (0, 1-2^-20] always passes, s >= 1+2^-20
+        // always fails (components are 0 or >= 2^-31 in magnitude, so s > 0 => len2 > 0); the sqrt and
+        // the division run once, after the loop, instead of on every try of every lane.
+        const float s2 = x * x + y * y + z * z;
+        bool acc = s2 > 0.0f && s2 <= 0.99999904632568359375f;           // 1 - 2^-20
+        if (!acc && s2 > 0.99999904632568359375f && s2 < 1.00000095367431640625f) {
+          const float l = sqrtf(s2);
+          acc = l * l <= 1.0f;
+        }
+        if (acc) { ruv = mk(x, y, z); break; }
       }
+      ruv = scale(1.0f / length(ruv), ruv);
       bool scattered = false;
       f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
       if (mkind == MAT_LAMBERTIAN) {                                        // :458-465
@@ -723,10 +737,17 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       if (scattered) {
         // push attenuation (the emission pushed with it is always 0: only lights emit and lights
         // never scatter, raytracing.cu:439-450 vs :457-488), so the unwind adds +0.0f per level
-        float *slot = A.rc + (static_cast<size_t>(depth) * 3) * A.threads + gtid;
-        slot[0] = att.x;
-        slot[A.threads] = att.y;
-        slot[2 * static_cast<size_t>(A.threads)] = att.z;
+        if (depth < A.rc_lds_levels) {
+          float *slot = rc_l + depth * 192;
+          slot[0] = att.x;
+          slot[64] = att.y;
+          slot[128] = att.z;
+        } else {
+          float *slot = A.rc + (static_cast<size_t>(depth) * 3) * A.threads + gtid;
+          slot[0] = att.x;
+          slot[A.threads] = att.y;
+          slot[2 * static_cast<size_t>(A.threads)] = att.z;
+        }
         depth++;
         if (COUNT) c_bounce++;
         ray.o = h.p;
@@ -742,9 +763,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     if (done) {
       for (int32_t k = static_cast<int32_t>(depth) - 1; k >= 0; --k) {      // :1362-1368
-        const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
-        res = mk(slot[0] * res.x + 0.0f, slot[A.threads] * res.y + 0.0f,
-                 slot[2 * static_cast<size_t>(A.threads)] * res.z + 0.0f);
+        f3 at;
+        if (static_cast<uint32_t>(k) < A.rc_lds_levels) {
+          const float *slot = rc_l + k * 192;
+          at = mk(slot[0], slot[64], slot[128]);
+        } else {
+          const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
+          at = mk(slot[0], slot[A.threads], slot[2 * static_cast<size_t>(A.threads)]);
+        }
+        res = mk(at.x * res.x + 0.0f, at.y * res.y + 0.0f, at.z * res.z + 0.0f);
       }
       sum = add(sum, res);
       sample++;

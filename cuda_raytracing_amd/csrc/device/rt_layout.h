@@ -69,11 +69,23 @@ enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket =
 // refill / traversal / shading
 constexpr uint32_t kWaveTraceWords = 9;
 
+// Resident 256-thread blocks per CU allowed by the VGPR budget: 512 VGPRs per lane per SIMD, one
+// wave of each block per SIMD.  The persistent grid must never exceed residency (a block that starts
+// late only lengthens the tail).  Measured on gfx950 with per-wave start stamps (tools/wave_trace.py):
+// kernels of 70 and 75 VGPRs ran 6 resident blocks/CU although the occupancy API reported 7, and
+// 80-86 VGPRs ran 5: consistent with an allocation granule of 16 for wave64, which is used here.
+inline int resident_blocks_by_vgprs(int vgprs) {
+  const int alloc = ((vgprs > 0 ? vgprs : 1) + 15) / 16 * 16;
+  const int w = 512 / alloc;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
 struct RenderArgs {
   const uint32_t *scene;      // compiled scene word image in HBM
   uint32_t scene_words;
   uint32_t off_mats, off_texs, off_perlin, off_pixels, pixel_words;
   uint32_t root, stack_cap, stack_lds_word;   // per-lane stack region starts at this LDS word
+  uint32_t rc_lds_word, rc_lds_levels;        // colour-stack levels [0, rc_lds_levels) live in LDS
   // camera (rt_camera)
   float p00[3], du[3], dv[3], center[3], dfu[3], dfv[3], defocus_angle;
   int32_t width, row_offset, row_stride;
@@ -94,12 +106,14 @@ struct RenderArgs {
   // Schedule.  A lane owns a pixel for all its samples (one XORWOW stream per pixel), so the frame
   // ends when the slowest pixels end: tiles are handed out longest-first (LPT) using a cheap probe.
   const uint32_t *tile_order;     // non-null: the t-th tile handed out is tile_order[t]
-  uint32_t *probe_cost;           // non-null: PROBE launch — kProbePerTile 1-spp paths per tile with
+  uint32_t probe_per_tile;        // probe paths per 8x8 tile (1..64)
+  uint32_t *probe_cost;           // non-null: PROBE launch — probe_per_tile 1-spp paths per tile with
                                   // a hashed RNG; adds each path's round count to probe_cost[tile]
   uint32_t reverse_tiles;         // no order array: 1 = hand tiles out bottom row first
 };
 
-constexpr uint32_t kProbePerTile = 8;   // probe paths per 8x8 tile
+constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
+constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)
 
 struct SeedArgs {
   const uint32_t *jump;       // xorwow_jump_tables() on device

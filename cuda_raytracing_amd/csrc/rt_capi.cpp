@@ -72,7 +72,7 @@ struct rt_context {
   int cu_count = 0;
   SceneImage img;
   DevBuf scene, jump, rng, rc, work, counters, wave_trace, tile_cost, tile_order;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
   bool counted = false;
   int variant = 0;
@@ -87,6 +87,8 @@ struct rt_context {
   size_t wave_trace_words = 0;
   int sched = 0;   // RT_SCHED: 0 auto (longest-first when spp >= kLptMinSpp), 1 row-major, 2 reversed, 3 longest-first
   int blocks_per_cu = 0;
+  uint32_t rc_lds_levels = rt::kRcLdsLevels;   // RT_RC_LDS_LEVELS
+  uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
   bool rendered = false;
   uint64_t samples = 0;
@@ -142,6 +144,9 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_BUDGET")) c->jit_budget = static_cast<uint32_t>(std::atoi(e));
   if (const char *e = std::getenv("RT_WAVE_TRACE")) c->wave_trace_path = e;
   if (const char *e = std::getenv("RT_SCHED")) c->sched = std::atoi(e);
+  if (const char *e = std::getenv("RT_PROBE"))
+    c->probe_per_tile = static_cast<uint32_t>(std::min(64, std::max(1, std::atoi(e))));
+  if (const char *e = std::getenv("RT_RC_LDS_LEVELS")) c->rc_lds_levels = static_cast<uint32_t>(std::atoi(e));
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
@@ -177,12 +182,13 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   c->samples = static_cast<uint64_t>(n) * static_cast<uint64_t>(p->samples_per_pixel);
   c->rendered = true;
   if (n == 0) {
-    (void)hipEventRecord(c->ev[0], s); (void)hipEventRecord(c->ev[1], s); (void)hipEventRecord(c->ev[2], s);
+    for (hipEvent_t e : c->ev) (void)hipEventRecord(e, s);
     return RT_OK;
   }
   if (mb == 0) {   // ray_color returns {0} without tracing (:1339): every pixel is exactly 0
     (void)hipEventRecord(c->ev[0], s);
     (void)hipEventRecord(c->ev[1], s);
+    (void)hipEventRecord(c->ev[3], s);
     if (hipMemsetAsync(out_dev, 0, static_cast<size_t>(n) * 12, s) != hipSuccess) return RT_ERR_HIP;
     (void)hipEventRecord(c->ev[2], s);
     return RT_OK;
@@ -191,8 +197,10 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   // launch geometry: persistent grid = resident blocks per CU x CUs
   c->lds = c->img.words.size() <= rt::kLdsSceneMaxWords && !(p->flags & RT_FLAG_GLOBAL_SCENE);
   const uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
+  const uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
+  const uint32_t rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
   const size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * c->img.stack_need * 64 * 2;
-  c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + stack_bytes;
+  c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
   // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
@@ -204,13 +212,13 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
   if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC)) trav = RT_TRAV_LANE;
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
-  hipFunction_t jit_fn = nullptr, jit_plain = nullptr;
+  hipFunction_t jit_fn = nullptr, jit_probe = nullptr;
   if (trav < 0 || trav == RT_TRAV_STATIC) {
     rt::JitKernels jk;
     std::string why;
     if (rt::jit_kernels(c->img, c->variant, c->jit_budget, &jk, &why)) {
       jit_fn = c->counted ? jk.render_count : jk.render;
-      jit_plain = jk.render;
+      jit_probe = jk.probe;
       c->jit_visits = jk.visits;
       trav = RT_TRAV_STATIC;
     } else {
@@ -219,7 +227,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     }
   }
   if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
-  if (jit_fn) c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4;   // straight-line traversal: no stacks
+  if (jit_fn) c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4;   // straight-line: no stacks
   c->used_traversal = trav;
   const int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes)
                             : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
@@ -248,7 +256,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.pixel_words = static_cast<uint32_t>(c->img.words.size()) - c->img.off_pixels;
   a.root = c->img.root;
   a.stack_cap = c->img.stack_need;
-  a.stack_lds_word = scene_lds_words;
+  a.rc_lds_word = scene_lds_words;
+  a.rc_lds_levels = rc_levels;
+  a.stack_lds_word = scene_lds_words + rc_lds_words;
   const rtr_vec3 *v3s[6] = {&cam->pixel00, &cam->delta_u, &cam->delta_v, &cam->center, &cam->defocus_u, &cam->defocus_v};
   float *dst[6] = {a.p00, a.du, a.dv, a.center, a.dfu, a.dfv};
   for (int k = 0; k < 6; ++k) { dst[k][0] = v3s[k]->x; dst[k][1] = v3s[k]->y; dst[k][2] = v3s[k]->z; }
@@ -288,7 +298,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   if (rt::launch_seed(sa, s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[1], s) != hipSuccess) return RT_ERR_HIP;
   if (c->used_lpt) {
-    // longest-first schedule: probe kProbePerTile throwaway 1-spp paths per tile (their own RNG,
+    // longest-first schedule: probe probe_per_tile throwaway 1-spp paths per tile (their own RNG,
     // no output), then counting-sort tiles by probe cost; counted in render_ms
     if (c->tile_cost.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess ||
         c->tile_order.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
@@ -296,13 +306,15 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     if (hipMemsetAsync(c->tile_cost.p, 0, static_cast<size_t>(n_tiles) * 4, s) != hipSuccess) return RT_ERR_HIP;
     rt::RenderArgs pa = a;
     pa.probe_cost = static_cast<uint32_t *>(c->tile_cost.p);
-    pa.n_ids = n_tiles * rt::kProbePerTile;
+    pa.probe_per_tile = c->probe_per_tile ? c->probe_per_tile
+                                          : static_cast<uint32_t>(std::min(64, std::max(8, p->samples_per_pixel / 4)));
+    pa.n_ids = n_tiles * pa.probe_per_tile;
     pa.spp = 1;
     pa.out = nullptr;
     pa.rng = nullptr;
     pa.work = static_cast<uint32_t *>(c->work.p) + 8;
     pa.wave_trace = nullptr;
-    const hipError_t pe = jit_plain ? rt::jit_launch(jit_plain, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
+    const hipError_t pe = jit_probe ? rt::jit_launch(jit_probe, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                     : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
                                                         c->lds_bytes, s);
     if (pe != hipSuccess) return RT_ERR_HIP;
@@ -310,6 +322,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
       return RT_ERR_HIP;
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
   }
+  if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
   if (le != hipSuccess) return RT_ERR_HIP;
@@ -327,11 +340,13 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   if (!c->rendered) return RT_OK;
   DeviceGuard g(c->device);
   if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;
-  float a = 0, b = 0;
+  float a = 0, b = 0, d = 0;
   if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) != hipSuccess) return RT_ERR_HIP;
-  if (hipEventElapsedTime(&b, c->ev[1], c->ev[2]) != hipSuccess) return RT_ERR_HIP;
+  if (hipEventElapsedTime(&b, c->ev[1], c->ev[3]) != hipSuccess) return RT_ERR_HIP;
+  if (hipEventElapsedTime(&d, c->ev[3], c->ev[2]) != hipSuccess) return RT_ERR_HIP;
   st->init_ms = a;
-  st->render_ms = b;
+  st->sched_ms = b;
+  st->render_ms = d;
   st->samples = c->samples;
   if (c->counted) {
     unsigned long long h[RT_CNT__COUNT];

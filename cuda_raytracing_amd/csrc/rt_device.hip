@@ -126,7 +126,10 @@ int render_blocks_per_cu(int variant, size_t lds_bytes) {
   if (variant < 0 || variant >= kKernels.n ||
       hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kKernels.ptr[variant], kBlock, lds_bytes) != hipSuccess || n <= 0)
     n = 1;
-  return n;
+  hipFuncAttributes fa;
+  if (variant >= 0 && variant < kKernels.n && hipFuncGetAttributes(&fa, kKernels.ptr[variant]) == hipSuccess)
+    n = min(n, resident_blocks_by_vgprs(fa.numRegs));
+  return n < 1 ? 1 : n;
 }
 
 }  // namespace rt

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <functional>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -41,6 +42,23 @@ std::string arch_of(int dev) {
 
 }  // namespace
 
+std::vector<std::string> jit_extra_options() {
+  std::vector<std::string> v;
+  if (const char *e = std::getenv("RT_JIT_OPTS")) {
+    std::string cur;
+    for (const char *p = e;; ++p) {
+      if (*p == ' ' || *p == '\0') {
+        if (!cur.empty()) v.push_back(cur);
+        cur.clear();
+        if (*p == '\0') break;
+      } else {
+        cur += *p;
+      }
+    }
+  }
+  return v;
+}
+
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::string *src, uint32_t *visits) {
   std::string trace;
   if (!generate_static_trace(img, max_visits, &trace, visits)) return false;
@@ -50,6 +68,8 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::st
          "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render_count(RenderArgs A) {\n"
          "  render_body<" + std::to_string(v | kVarCount) + ", StaticTrace>(A);\n}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void rt_static_probe(RenderArgs A) {\n"
+         "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
          "}  // namespace rt\n";
   return true;
 }
@@ -62,10 +82,16 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
     if (log) *log = "hiprtcCreateProgram failed";
     return false;
   }
-  const std::string arch_opt = "--offload-arch=" + arch;
-  const char *opts[] = {arch_opt.c_str(), "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                        "-fhip-fp32-correctly-rounded-divide-sqrt"};
-  const hiprtcResult r = hiprtcCompileProgram(prog, 6, opts);
+  // Same numerics flags as the offline build.  SLP vectorisation is off: on this code it packs
+  // scalar f32 pairs into v_pk_* with extra moves, turns the planar inside-test into a <4 x i1>
+  // reduction, and its longer live ranges spill ~100 SGPRs (measured: -10% instructions, 86 -> 71
+  // VGPRs on scene 0).  RT_JIT_OPTS appends options (A/B experiments).
+  std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                                "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
+  for (const std::string &x : jit_extra_options()) o.push_back(x);
+  std::vector<const char *> opts;
+  for (const std::string &x : o) opts.push_back(x.c_str());
+  const hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(opts.size()), opts.data());
   bool ok = r == HIPRTC_SUCCESS;
   if (log) {
     size_t n = 0;
@@ -100,7 +126,9 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKer
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const std::string arch = arch_of(dev);
-  const std::string key = arch + "|" + std::to_string(dev) + "|" + src;
+  std::string key = arch + "|" + std::to_string(dev) + "|";
+  for (const std::string &x : jit_extra_options()) key += x + " ";
+  key += "|" + src;
   std::lock_guard<std::mutex> lock(g_mu);
   auto it = g_cache.find(key);
   if (it == g_cache.end()) {
@@ -111,7 +139,8 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKer
       e->why = "hipRTC compile failed: " + log.substr(0, 2000);
     } else if (hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
                hipModuleGetFunction(&e->k.render, e->mod, "rt_static_render") != hipSuccess ||
-               hipModuleGetFunction(&e->k.render_count, e->mod, "rt_static_render_count") != hipSuccess) {
+               hipModuleGetFunction(&e->k.render_count, e->mod, "rt_static_render_count") != hipSuccess ||
+               hipModuleGetFunction(&e->k.probe, e->mod, "rt_static_probe") != hipSuccess) {
       e->why = "hipModuleLoadData/GetFunction failed";
     } else {
       e->ok = true;
@@ -136,7 +165,14 @@ hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, si
 int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes) {
   int n = 0;
   if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, lds_bytes) != hipSuccess || n <= 0) n = 1;
-  return n;
+  int vgprs = 0;
+  const hipError_t e = hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, fn);
+  const int api = n;
+  if (e == hipSuccess) n = std::min(n, resident_blocks_by_vgprs(vgprs));
+  if (std::getenv("RT_DEBUG"))
+    std::fprintf(stderr, "[rt] jit occupancy: api %d blocks/CU, NUM_REGS %d (%s) -> %d, lds %zu B\n", api, vgprs,
+                 hipGetErrorString(e), n, lds_bytes);
+  return std::max(n, 1);
 }
 
 }  // namespace rt

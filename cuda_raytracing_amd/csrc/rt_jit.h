@@ -12,6 +12,7 @@ namespace rt {
 struct JitKernels {
   hipFunction_t render = nullptr;        // StaticTrace, no counters
   hipFunction_t render_count = nullptr;  // StaticTrace, counters
+  hipFunction_t probe = nullptr;         // StaticTrace, schedule probe launches (same body, own symbol)
   uint32_t visits = 0;                   // node visits in the expanded traversal
 };
 
@@ -25,6 +26,9 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKer
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::string *src, uint32_t *visits);
 // Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
+
+// extra hipRTC options from the RT_JIT_OPTS environment variable (space separated)
+std::vector<std::string> jit_extra_options();
 
 hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes);

@@ -111,6 +111,7 @@ typedef struct rt_stats {
   int32_t scene_in_lds;    /* 1 if the compiled scene was staged in LDS */
   int32_t traversal;       /* RT_TRAV_* used by the last render */
   int32_t jit_visits;      /* node visits of the specialised traversal (RT_TRAV_STATIC) */
+  double sched_ms;         /* longest-first schedule: probe paths + tile sort, before the render kernel */
 } rt_stats;
 
 /* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of

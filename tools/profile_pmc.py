@@ -27,12 +27,17 @@ def main():
     out = Path(args[args.index("--out") + 1]) if "--out" in args else Path("gpurun_out/pmc")
     if "--out" in args:
         i = args.index("--out"); del args[i:i + 2]
+    passes = PASSES
+    if "--sets" in args:   # custom passes: "A,B;C,D"
+        i = args.index("--sets")
+        passes = [x.split(",") for x in args[i + 1].split(";")]
+        del args[i:i + 2]
     out = out.resolve()
     out.mkdir(parents=True, exist_ok=True)
     repo = Path(__file__).resolve().parents[1]
     env = dict(os.environ, TMPDIR="/tmp")
     summary = {"workload": args, "passes": []}
-    for k, counters in enumerate(PASSES):
+    for k, counters in enumerate(passes):
         d = out / f"pass{k}"
         cmd = ["rocprofv3", "--kernel-trace", "--pmc", *counters, "--output-format", "csv", "-d", str(d), "-o", "run",
                "--", sys.executable, str(repo / "tools" / "pmc_workload.py"), *args]

@@ -1,6 +1,6 @@
 """A/B render-context options (env knobs read at context creation) in ONE process, interleaved rounds (guide §5.4 rule 24).
 
-Every configuration must produce a bit-identical frame (the schedule never changes what a lane
+Times are render + schedule (probe and tile sort) kernel time.  Every configuration must produce a bit-identical frame (the schedule never changes what a lane
 computes); the script asserts that and prints median render ms per configuration.
     python3 tools/tune.py --scene 0 --spp 64 --configs RT_TRAVERSAL=0,RT_TRAVERSAL=1 --rounds 3
 """
@@ -47,7 +47,7 @@ for r in range(a.rounds + 1):
             ref = img.copy()
         assert np.array_equal(img, ref), f"config {c} changed the frame"
         if r > 0:
-            times[c].append(t.render_ms)
+            times[c].append(t.render_ms + t.sched_ms)
 res = {c: {"median_ms": statistics.median(v), "min_ms": min(v),
            "msamples_s": W * H * a.spp / statistics.median(v) / 1e3} for c, v in times.items()}
 for c, v in sorted(res.items(), key=lambda kv: kv[1]["median_ms"]):
