@@ -15,14 +15,14 @@ import numpy as np
 from . import _abi
 from ._abi import (Camera, Params, Scene, Settings, Stats, Vec3, vec3, RT_FLAG_COUNT,
                    RT_FLAG_GLOBAL_SCENE, RT_FLAG_NO_JIT, RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET,
-                   RT_FLAG_FORCE_STATIC, RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
+                   RT_FLAG_FORCE_STATIC, RT_FLAG_NO_FOLD, RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
                    RT_XF_TRANSLATE, RT_XF_YROTATE, RT_XF_YROTATE_TRANSLATE)
 
 __all__ = [
     "World", "Camera", "Params", "Scene", "Settings", "Stats", "vec3", "build_scene",
     "camera_from_settings", "make_params", "render", "RenderContext", "tonemap", "write_ppm",
     "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE",
-    "RT_FLAG_NO_JIT", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_TRAV_LANE",
+    "RT_FLAG_NO_JIT", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_TRAV_LANE",
     "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError",
 ]

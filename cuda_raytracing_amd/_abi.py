@@ -28,6 +28,7 @@ RT_FLAG_COUNT = 0x1
 RT_FLAG_GLOBAL_SCENE = 0x2
 RT_FLAG_NO_JIT = 0x4
 RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET, RT_FLAG_FORCE_STATIC = 0x8, 0x10, 0x20
+RT_FLAG_NO_FOLD = 0x40
 RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC = 0, 1, 2
 
 CNT_NAMES = [
@@ -91,6 +92,7 @@ class Stats(C.Structure):
         ("stack_needed", C.c_int32), ("scene_in_lds", C.c_int32),
         ("traversal", C.c_int32), ("jit_visits", C.c_int32),
         ("sched_ms", C.c_double),
+        ("folded", C.c_int32), ("fold_rerenders", C.c_int32),
     ]
 
     def counter_dict(self):

@@ -302,6 +302,40 @@ __device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32
   }
 }
 
+// sphere with a constant centre (scene_codegen.cpp folds c + mv*time when mv = +-0)
+template <bool UV>
+__device__ __forceinline__ void sphere_hit_static(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 center, float rad2,
+                                                  float inv_rad, bool in_xf) {
+  f3 oc = sub(center, r.o);
+  float a = dot(r.d, r.d);
+  float b = -2.0f * dot(r.d, oc);
+  float c = dot(oc, oc) - rad2;
+  float disc = b * b - 4 * a * c;
+  if (disc >= 0) {
+    float sq = sqrtf(disc);
+    float root = (-b - sq) / (2.0f * a);
+    if (kTmin >= root || root >= T.tmax) root = (-b + sq) / (2.0f * a);
+    if (kTmin < root && root < T.tmax) {
+      h.t = root;
+      h.p = line_at(r.o, root, r.d);
+      h.mat = mat;
+      f3 outward = scale(inv_rad, sub(h.p, center));
+      if (UV) {
+        const float pi = 3.1415926535897932385f;
+        float theta = acosf(-outward.y);
+        float phi = atan2f(-outward.z, outward.x) + pi;
+        h.u = phi / (2 * pi);
+        h.v = theta / pi;
+      }
+      h.front = dot(r.d, outward) < 0;
+      h.n = h.front ? outward : flip(outward);
+      T.tmax = h.t;
+      T.result = true;
+      if (in_xf) T.was_last = true;
+    }
+  }
+}
+
 // translation enter / cleanup (:1176-1191)
 __device__ __forceinline__ void translate_enter(Trav &T, Ray &r, f3 off) {
   T.was_last = false;

@@ -110,6 +110,7 @@ struct RenderArgs {
   uint32_t *probe_cost;           // non-null: PROBE launch — probe_per_tile 1-spp paths per tile with
                                   // a hashed RNG; adds each path's round count to probe_cost[tile]
   uint32_t reverse_tiles;         // no order array: 1 = hand tiles out bottom row first
+  uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

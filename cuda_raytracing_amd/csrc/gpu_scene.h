@@ -31,7 +31,9 @@ int compile_scene(const void *scene /* const rt_scene* */, SceneImage *out);
 
 // Scene-specialised traversal: HIP source of `struct StaticTrace` (the scene's DFS expanded into
 // straight-line code with node data as immediates).  Returns false when the expansion would exceed
-// max_visits node visits (large scenes keep the generic kernels).
-bool generate_static_trace(const SceneImage &img, uint32_t max_visits, std::string *src, uint32_t *visits);
+// max_visits node visits (large scenes keep the generic kernels).  fold: emit the exactly-folded
+// primitive tests (scene_codegen.cpp header); *folded reports whether folding was applied.
+bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
+                           bool *folded);
 
 }  // namespace rt

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -65,7 +66,43 @@ static_assert(rt::CNT_BOUNCES == RT_CNT_BOUNCES && rt::CNT_SHADES == RT_CNT_SHAD
               rt::CNT_OVERFLOW == RT_CNT_STACK_OVERFLOW && rt::CNT_SLOTS == RT_CNT__COUNT, "counter slots");
 static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::K_GROUP == RTR_OBJ_GROUP, "kinds");
 
-constexpr int kLptMinSpp = 16;   // the probe costs 8 paths per 64-pixel tile: <1% of the frame from here
+constexpr int kLptMinSpp = 16;
+constexpr float kFoldRayBound = 1.0e6f;   // fold only when every ray provably stays below this
+
+// Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
+// precondition, scene_codegen.cpp).  Primary rays: camera centre + lens offset, directions to the
+// viewport.  Secondary rays start on a primitive, inside the root BVH box, and leave in a direction
+// of length <= 2 + fuzz (Lambertian n + unit, metal unit + fuzz*unit, dielectric reflect/refract of
+// unit vectors).  Returns +inf when no bound is available (root is not a BVH node).
+float ray_bound(const rt::SceneImage &img, const rt_camera *cam, const rt_params *p) {
+  auto ab = [](float x) { return std::fabs(x); };
+  const rtr_vec3 *c0 = &cam->center, *fu = &cam->defocus_u, *fv = &cam->defocus_v;
+  const float ox = ab(c0->x) + ab(fu->x) + ab(fv->x), oy = ab(c0->y) + ab(fu->y) + ab(fv->y),
+              oz = ab(c0->z) + ab(fu->z) + ab(fv->z);
+  const float W = static_cast<float>(p->width), H = static_cast<float>(p->height);
+  const float dx = ab(cam->pixel00.x) + (W + 1) * ab(cam->delta_u.x) + (H + 1) * ab(cam->delta_v.x) + ox;
+  const float dy = ab(cam->pixel00.y) + (W + 1) * ab(cam->delta_u.y) + (H + 1) * ab(cam->delta_v.y) + oy;
+  const float dz = ab(cam->pixel00.z) + (W + 1) * ab(cam->delta_u.z) + (H + 1) * ab(cam->delta_v.z) + oz;
+  float b = std::max({ox, oy, oz, dx, dy, dz});
+  const uint32_t *root = &img.words[static_cast<size_t>(img.root) * rt::kNodeWords];
+  if (root[rt::W_KIND] != rt::K_BVH) return INFINITY;
+  for (int k = 0; k < 6; ++k) {
+    float v;
+    std::memcpy(&v, &root[rt::W_BOX + k], 4);
+    b = std::max(b, 2.0f * ab(v) + 1.0f);
+  }
+  float fuzz = 0.0f;
+  for (uint32_t m = 0; m < img.mat_count; ++m) {
+    const uint32_t *mw = &img.words[img.off_mats + static_cast<size_t>(m) * rt::kMatWords];
+    if (mw[rt::M_KIND] == rt::MAT_METAL) {
+      float f;
+      std::memcpy(&f, &mw[rt::M_FUZZ], 4);
+      fuzz = std::max(fuzz, ab(f));
+    }
+  }
+  b = std::max(b, 3.0f + fuzz);
+  return std::isfinite(b) ? b : INFINITY;
+}   // the probe costs 8 paths per 64-pixel tile: <1% of the frame from here
 
 struct rt_context {
   int device = 0;
@@ -90,6 +127,14 @@ struct rt_context {
   uint32_t rc_lds_levels = rt::kRcLdsLevels;   // RT_RC_LDS_LEVELS
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
+  bool fold_enabled = true;
+  uint32_t fold_violations = 0;      // RT_JIT_FOLD=0 disables exact constant folding (A/B)
+  bool used_fold = false;
+  // the last render, for the unfolded re-render after a fold-bound violation (rt_context_timing)
+  rt_camera last_cam{};
+  rt_params last_params{};
+  float *last_out = nullptr;
+  void *last_stream = nullptr;
   bool rendered = false;
   uint64_t samples = 0;
   size_t lds_bytes = 0;
@@ -127,6 +172,7 @@ void rt_context_destroy(rt_context *c) {
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
     c->scene.release(); c->jump.release(); c->rng.release(); c->rc.release();
     c->work.release(); c->counters.release();
+    c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
   }
   delete c;
 }
@@ -144,6 +190,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_BUDGET")) c->jit_budget = static_cast<uint32_t>(std::atoi(e));
   if (const char *e = std::getenv("RT_WAVE_TRACE")) c->wave_trace_path = e;
   if (const char *e = std::getenv("RT_SCHED")) c->sched = std::atoi(e);
+  if (const char *e = std::getenv("RT_JIT_FOLD")) c->fold_enabled = e[0] != '0';
   if (const char *e = std::getenv("RT_PROBE"))
     c->probe_per_tile = static_cast<uint32_t>(std::min(64, std::max(1, std::atoi(e))));
   if (const char *e = std::getenv("RT_RC_LDS_LEVELS")) c->rc_lds_levels = static_cast<uint32_t>(std::atoi(e));
@@ -213,10 +260,14 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC)) trav = RT_TRAV_LANE;
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
   hipFunction_t jit_fn = nullptr, jit_probe = nullptr;
+  c->used_fold = false;
   if (trav < 0 || trav == RT_TRAV_STATIC) {
     rt::JitKernels jk;
     std::string why;
-    if (rt::jit_kernels(c->img, c->variant, c->jit_budget, &jk, &why)) {
+    const bool want_fold = c->fold_enabled && !(p->flags & RT_FLAG_NO_FOLD) &&
+                           ray_bound(c->img, cam, p) <= kFoldRayBound;
+    if (rt::jit_kernels(c->img, c->variant, c->jit_budget, want_fold, &jk, &why)) {
+      c->used_fold = jk.folded;
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
       c->jit_visits = jk.visits;
@@ -281,6 +332,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.tile_order = nullptr;
   a.probe_cost = nullptr;
   a.reverse_tiles = c->sched == 2 ? 1u : 0u;
+  a.fold_violation = static_cast<uint32_t *>(c->work.p) + 15;   // zeroed with the work counters
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;
@@ -314,6 +366,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     pa.rng = nullptr;
     pa.work = static_cast<uint32_t *>(c->work.p) + 8;
     pa.wave_trace = nullptr;
+    pa.fold_violation = static_cast<uint32_t *>(c->work.p) + 14;   // probe rays: flag ignored
     const hipError_t pe = jit_probe ? rt::jit_launch(jit_probe, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                     : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
                                                         c->lds_bytes, s);
@@ -327,6 +380,10 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
   if (le != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
+  c->last_cam = *cam;
+  c->last_params = *p;
+  c->last_out = out_dev;
+  c->last_stream = stream;
   return RT_OK;
 }
 
@@ -337,9 +394,25 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->scene_in_lds = c->lds ? 1 : 0;
   st->traversal = c->used_traversal;
   st->jit_visits = static_cast<int32_t>(c->jit_visits);
+  st->folded = c->used_fold ? 1 : 0;
+  st->fold_rerenders = static_cast<int32_t>(c->fold_violations);
   if (!c->rendered) return RT_OK;
   DeviceGuard g(c->device);
   if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;
+  if (c->used_fold) {
+    // a ray outside the host's bound voids the folding precondition: render the frame again unfolded
+    uint32_t v = 0;
+    if (hipMemcpy(&v, static_cast<uint32_t *>(c->work.p) + 15, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      return RT_ERR_HIP;
+    if (v) {
+      c->fold_violations++;
+      rt_params q = c->last_params;
+      q.flags |= RT_FLAG_NO_FOLD;
+      const int rc = rt_context_render(c, &c->last_cam, &q, c->last_out, c->last_stream);
+      if (rc != RT_OK) return rc;
+      return rt_context_timing(c, st);
+    }
+  }
   float a = 0, b = 0, d = 0;
   if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) != hipSuccess) return RT_ERR_HIP;
   if (hipEventElapsedTime(&b, c->ev[1], c->ev[3]) != hipSuccess) return RT_ERR_HIP;
@@ -410,7 +483,7 @@ int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint
   std::string src;
   uint32_t v = 0;
   const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0);
-  const bool ok = rt::jit_source(img, variant, max_visits, &src, &v);
+  const bool ok = rt::jit_source(img, variant, max_visits, true, &src, &v);
   if (visits) *visits = v;
   if (!ok) return RT_ERR_UNSUPPORTED;
   copy_out(src, buf, cap);
@@ -425,7 +498,7 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
   std::string src, lg;
   uint32_t v = 0;
   const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0);
-  if (!rt::jit_source(img, variant, max_visits, &src, &v)) return RT_ERR_UNSUPPORTED;
+  if (!rt::jit_source(img, variant, max_visits, true, &src, &v)) return RT_ERR_UNSUPPORTED;
   std::vector<char> code;
   const bool ok = rt::jit_compile(src, arch, &code, &lg);
   copy_out(lg, log, cap);

@@ -59,9 +59,10 @@ std::vector<std::string> jit_extra_options() {
   return v;
 }
 
-bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::string *src, uint32_t *visits) {
+bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
+                bool *folded) {
   std::string trace;
-  if (!generate_static_trace(img, max_visits, &trace, visits)) return false;
+  if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
   const int v = variant & (kVarLds | kVarNoise | kVarUv);
   *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
          "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render(RenderArgs A) {\n"
@@ -116,10 +117,11 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
   return ok;
 }
 
-bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKernels *out, std::string *why) {
+bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
   std::string src;
   uint32_t visits = 0;
-  if (!jit_source(img, variant, max_visits, &src, &visits)) {
+  bool folded = false;
+  if (!jit_source(img, variant, max_visits, fold, &src, &visits, &folded)) {
     if (why) *why = "scene expansion exceeds " + std::to_string(max_visits) + " node visits";
     return false;
   }
@@ -145,6 +147,7 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKer
     } else {
       e->ok = true;
       e->k.visits = visits;
+      e->k.folded = folded;
     }
     it = g_cache.emplace(key, std::move(e)).first;
   }

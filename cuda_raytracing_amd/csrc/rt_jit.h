@@ -14,16 +14,18 @@ struct JitKernels {
   hipFunction_t render_count = nullptr;  // StaticTrace, counters
   hipFunction_t probe = nullptr;         // StaticTrace, schedule probe launches (same body, own symbol)
   uint32_t visits = 0;                   // node visits in the expanded traversal
+  bool folded = false;                   // primitive tests exactly folded (scene_codegen.cpp)
 };
 
 // Compile (or fetch from the process-wide cache) the StaticTrace kernels of `img` for `variant`
 // (kVarLds | kVarNoise | kVarUv bits) on the current device.  Returns false (and a reason in *why)
 // when the scene is too large for the expansion budget or hipRTC is unavailable / fails: callers
 // then keep the generic kernels.
-bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, JitKernels *out, std::string *why);
+bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why);
 
 // Full hipRTC source of the StaticTrace kernels for `variant` (no device needed).
-bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, std::string *src, uint32_t *visits);
+bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
+                bool *folded = nullptr);
 // Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
 

@@ -12,7 +12,27 @@
 // so the whole traversal of a small scene can be emitted as nested ifs with every node constant as an
 // immediate: no stack, no node loads, no kind dispatch, and per-visit work identical to the generic
 // kernels (the same planar_hit / sphere_hit / box_hit / transform helpers of device/rt_body.h).
+//
+// Exact constant folding (the "folded" copy of the traversal).  With node data known, many products
+// in the quad/triangle test multiply by +-0 or +-1 (axis-aligned normals, edges, origins).  Only
+// rewrites that give bit-identical results are applied:
+//   x * 1 -> x,  x * -1 -> -x,  x - (+0) -> x          exact for every x;
+//   a + x*(+-0), a - x*(+-0) -> a                      exact for FINITE x, up to the sign of a zero
+//                                                      result (a left-to-right sum that drops +-0
+//                                                      terms equals the original except that a zero
+//                                                      result may differ in sign);
+// and every folded value only feeds zero-sign-insensitive consumers: |denom| >= eps, t = num/denom
+// (a zero num gives t = +-0 < tmin either way), the inside compares, front = denom < 0, and — only
+// when no image texture reads u,v — alpha/beta stored as h.u/h.v.  Sphere centres with zero motion
+// fold to constants (time is in (0,1], so mv*time == mv for mv = +-0).  Finiteness: the folded copy
+// is used only when every ray has |o|,|d| <= 1e9 at traversal start; with the scene's constants bounded by 1e6 (checked here, else no folding) every
+// dropped factor (d, o, p - q, the edge cross products) stays finite through <= 2 transform levels.
+// The host decides per render whether every ray is bounded (rt_capi.cpp ray_bound()); the kernel
+// double-checks each traversal and flags violations (the frame is then re-rendered unfolded).
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "gpu_scene.h"
@@ -20,13 +40,111 @@
 namespace rt {
 namespace {
 
+// an emitted scalar expression; zero = the value is +-0 (sign unknown, only in folded code)
+struct E {
+  std::string s;
+  bool zero = false;
+};
+
 struct Gen {
   const SceneImage &img;
   uint32_t budget;
+  bool fold = false;          // emit the folded copy
+  bool fold_uv = false;       // alpha/beta may be folded too (no image texture reads u,v)
   std::string out;
   uint32_t visits = 0;
   int indent = 4;
   bool ok = true;
+  uint32_t uid = 0;
+
+  static bool is_zero(uint32_t b) { return (b & 0x7fffffffu) == 0; }
+  // c * x (x a runtime value, finite in folded code)
+  E term(const E &x, uint32_t cbits, bool fold_here) const {
+    if (x.zero && fold_here) return E{"", true};
+    if (fold_here && is_zero(cbits)) return E{"", true};
+    if (fold_here && cbits == 0x3f800000u) return x;
+    if (fold_here && cbits == 0xbf800000u) return E{"(-" + x.s + ")", false};
+    return E{"(" + x.s + " * " + f(cbits) + ")", false};
+  }
+  static E sum(const E &a, const E &b) {
+    if (a.zero) return b;
+    if (b.zero) return a;
+    return E{"(" + a.s + " + " + b.s + ")", false};
+  }
+  static E diff(const E &a, const E &b) {
+    if (b.zero) return a;
+    if (a.zero) return E{"(-" + b.s + ")", false};
+    return E{"(" + a.s + " - " + b.s + ")", false};
+  }
+  static std::string val(const E &e) { return e.zero ? std::string("0.0f") : e.s; }
+  // dot(c, x) = (c.x*x.x + c.y*x.y) + c.z*x.z with constant c (product order is immaterial)
+  E dotc(const uint32_t *c, const E x[3], bool fold_here) const {
+    return sum(sum(term(x[0], c[0], fold_here), term(x[1], c[1], fold_here)), term(x[2], c[2], fold_here));
+  }
+
+  // quad / triangle test (planar_hit in device/rt_body.h) with exact folding
+  void planar_folded(const uint32_t *w, bool tri, bool in_xf, uint32_t i) {
+    const std::string k = std::to_string(uid++);
+    const E d[3] = {{"r.d.x"}, {"r.d.y"}, {"r.d.z"}}, o[3] = {{"r.o.x"}, {"r.o.y"}, {"r.o.z"}};
+    const E den = dotc(w + W_NORMAL, d, true);
+    const E non = dotc(w + W_NORMAL, o, true);
+    line("{   // node " + u(i) + (tri ? " (triangle, folded)" : " (quad, folded)"));
+    indent += 2;
+    line("const float den" + k + " = " + val(den) + ";");
+    line("if (fabsf(den" + k + ") >= kDenomEps) {");
+    indent += 2;
+    line("const float t" + k + " = (" + f(w[W_D]) + " - " + val(non) + ") / den" + k + ";");
+    line("if (kTmin <= t" + k + " && t" + k + " <= T.tmax) {");
+    indent += 2;
+    line("const f3 p" + k + " = mk(r.o.x + r.d.x * t" + k + ", r.o.y + r.d.y * t" + k + ", r.o.z + r.d.z * t" + k + ");");
+    const char *ax[3] = {"x", "y", "z"};
+    E pq[3];
+    for (int a = 0; a < 3; ++a) {
+      const uint32_t qb = w[W_Q + a];
+      pq[a] = E{qb == 0u ? "p" + k + "." + ax[a] : "(p" + k + "." + ax[a] + " - " + f(qb) + ")", false};
+    }
+    for (int a = 0; a < 3; ++a) line("const float q" + k + ax[a] + " = " + pq[a].s + ";");
+    const E qv[3] = {{"q" + k + "x"}, {"q" + k + "y"}, {"q" + k + "z"}};
+    const uint32_t *vv = w + W_V, *uu = w + W_U, *ww = w + W_W;
+    const bool fa = fold_uv;
+    // cross(pq, vv) and cross(uu, pq) as in rt_body.h cross()
+    const E c1[3] = {diff(term(qv[1], vv[2], fa), term(qv[2], vv[1], fa)),
+                     diff(term(qv[2], vv[0], fa), term(qv[0], vv[2], fa)),
+                     diff(term(qv[0], vv[1], fa), term(qv[1], vv[0], fa))};
+    const E c2[3] = {diff(term(qv[2], uu[1], fa), term(qv[1], uu[2], fa)),
+                     diff(term(qv[0], uu[2], fa), term(qv[2], uu[0], fa)),
+                     diff(term(qv[1], uu[0], fa), term(qv[0], uu[1], fa))};
+    // the reference forms uu.y*pq.z - uu.z*pq.y: term() writes (pq.z * uu.y), the same product
+    for (int a = 0; a < 3; ++a) {
+      if (!c1[a].zero) line("const float a" + k + ax[a] + " = " + c1[a].s + ";");
+      if (!c2[a].zero) line("const float b" + k + ax[a] + " = " + c2[a].s + ";");
+    }
+    E ca[3], cb[3];
+    for (int a = 0; a < 3; ++a) {
+      ca[a] = c1[a].zero ? E{"", true} : E{std::string("a") + k + ax[a], false};
+      cb[a] = c2[a].zero ? E{"", true} : E{std::string("b") + k + ax[a], false};
+    }
+    const E al = dotc(ww, ca, fa), be = dotc(ww, cb, fa);
+    line("const float al" + k + " = " + val(al) + ", be" + k + " = " + val(be) + ";");
+    std::string in = "(0.0f <= al" + k + ") & (al" + k + " <= 1.0f) & (0.0f <= be" + k + ") & (be" + k + " <= 1.0f)";
+    if (tri) in += " & (al" + k + " + be" + k + " <= 1.0f)";
+    line("if (" + in + ") {");
+    indent += 2;
+    const uint32_t *n = w + W_NORMAL;
+    line("h.u = al" + k + "; h.v = be" + k + "; h.t = t" + k + "; h.p = p" + k + "; h.mat = " + u(w[W_AUX]) + ";");
+    line("h.front = den" + k + " < 0.0f;");
+    line("h.n = h.front ? " + v3(w, W_NORMAL) + " : mk(" + f(n[0] ^ 0x80000000u) + ", " + f(n[1] ^ 0x80000000u) + ", " +
+         f(n[2] ^ 0x80000000u) + ");");
+    line(std::string("T.tmax = t") + k + "; T.result = true;" + (in_xf ? " T.was_last = true;" : ""));
+    indent -= 2;
+    line("}");
+    indent -= 2;
+    line("}");
+    indent -= 2;
+    line("}");
+    indent -= 2;
+    line("}");
+  }
 
   const uint32_t *node(uint32_t i) const { return &img.words[static_cast<size_t>(i) * kNodeWords]; }
   static std::string f(uint32_t bits) {
@@ -61,15 +179,32 @@ struct Gen {
       case K_QUAD:
       case K_TRIANGLE:
         line("if (COUNT) vc.k[" + u(w[W_KIND]) + "]++;");
+        if (fold) { planar_folded(w, w[W_KIND] == K_TRIANGLE, in_t || in_r, i); break; }
         line(std::string("planar_hit(T, r, h, ") + (w[W_KIND] == K_TRIANGLE ? "true" : "false") + ", " + u(w[W_AUX]) +
              ", " + v3(w, W_NORMAL) + ", " + f(w[W_D]) + ", " + v3(w, W_Q) + ", " + v3(w, W_U) + ", " + v3(w, W_V) +
              ", " + v3(w, W_W) + ", " + xf + ");   // node " + u(i));
         break;
-      case K_SPHERE:
+      case K_SPHERE: {
         line("if (COUNT) vc.k[" + u(K_SPHERE) + "]++;");
+        const uint32_t *mv = w + W_MOTION;
+        if (fold && is_zero(mv[0]) && is_zero(mv[1]) && is_zero(mv[2])) {
+          // centre(t) = c + mv*t with mv = +-0 and t in (0,1]: exactly c + mv (float add, sign rules)
+          uint32_t cb[3];
+          for (int a = 0; a < 3; ++a) {
+            float c, m, r;
+            std::memcpy(&c, &w[W_CENTER + a], 4);
+            std::memcpy(&m, &mv[a], 4);
+            r = c + m;
+            std::memcpy(&cb[a], &r, 4);
+          }
+          line("sphere_hit_static<UV>(T, r, h, " + u(w[W_AUX]) + ", mk(" + f(cb[0]) + ", " + f(cb[1]) + ", " + f(cb[2]) +
+               "), " + f(w[W_RADIUS2]) + ", " + f(w[W_INV_RADIUS]) + ", " + xf + ");   // node " + u(i) + " (folded)");
+          break;
+        }
         line("sphere_hit<UV>(T, r, h, " + u(w[W_AUX]) + ", " + v3(w, W_CENTER) + ", " + v3(w, W_MOTION) + ", " +
              f(w[W_RADIUS2]) + ", " + f(w[W_INV_RADIUS]) + ", " + xf + ");   // node " + u(i));
         break;
+      }
       case K_TRANSLATE:
         if (in_t) { ok = false; return; }
         line("if (COUNT) vc.k[" + u(K_TRANSLATE) + "]++;");
@@ -98,18 +233,55 @@ struct Gen {
 
 }  // namespace
 
-bool generate_static_trace(const SceneImage &img, uint32_t max_visits, std::string *src, uint32_t *visits) {
+// Scene constants small enough for the finiteness argument of the folded copy (header comment).
+bool foldable(const SceneImage &img) {
+  auto small = [](uint32_t b) {
+    float x;
+    std::memcpy(&x, &b, 4);
+    return std::fabs(x) <= 1.0e6f;   // false for inf / NaN
+  };
+  for (uint32_t i = 0; i < img.node_count; ++i) {
+    const uint32_t *w = &img.words[static_cast<size_t>(i) * kNodeWords];
+    if (w[W_KIND] == K_QUAD || w[W_KIND] == K_TRIANGLE) {
+      for (int k = W_NORMAL; k < W_W; ++k) if (!small(w[k])) return false;
+      for (int k = W_W; k < W_W + 3; ++k) {
+        float x;
+        std::memcpy(&x, &w[k], 4);
+        if (!std::isfinite(x)) return false;
+      }
+    } else if (w[W_KIND] == K_TRANSLATE) {
+      for (int k = 0; k < 3; ++k) if (!small(w[W_OFFSET + k])) return false;
+    }
+  }
+  return true;
+}
+
+bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
+                           bool *folded) {
+  fold = fold && foldable(img);
   Gen g{img, max_visits};
+  g.fold = fold;
+  g.fold_uv = fold && !img.needs_uv;
   g.walk(img.root, false, false, 0);
   if (visits) *visits = g.visits;
+  if (folded) *folded = fold;
   if (!g.ok) return false;
   src->clear();
   *src += "struct StaticTrace {\n";
   *src += "  template <bool LDS, bool COUNT, bool UV>\n";
-  *src += "  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &, bool busy, uint64_t,\n";
+  *src += "  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &A, bool busy, uint64_t,\n";
   *src += "                                             uint32_t, uint16_t *, Trav &T, Ray &r, Hit &h, Visits &vc) {\n";
   *src += "    if (!busy) return;\n";
   *src += "    trav_reset(T, r);\n";
+  if (fold) {
+    // the host enables folding only when it can bound every ray by 1e6 (camera + scene box + materials);
+    // a lane that ever sees a larger or non-finite ray flags the frame, which the host then re-renders
+    // without folding (rt_context_timing), so a wrong bound can cost time but never change a frame
+    *src += "    const float kB = 1.0e9f;\n";
+    *src += "    const bool small = (fabsf(r.o.x) <= kB) & (fabsf(r.o.y) <= kB) & (fabsf(r.o.z) <= kB) &\n";
+    *src += "                       (fabsf(r.d.x) <= kB) & (fabsf(r.d.y) <= kB) & (fabsf(r.d.z) <= kB);\n";
+    *src += "    if (!small) atomicOr(A.fold_violation, 1u);\n";
+  }
   *src += g.out;
   *src += "  }\n};\n";
   return true;

@@ -81,6 +81,7 @@ typedef struct rt_params {
 #define RT_FLAG_FORCE_LANE   0x8u  /* force RT_TRAV_LANE   (A/B and parity tests; default: auto) */
 #define RT_FLAG_FORCE_PACKET 0x10u /* force RT_TRAV_PACKET (falls back to LANE if the stack is too deep) */
 #define RT_FLAG_FORCE_STATIC 0x20u /* force RT_TRAV_STATIC (falls back to LANE over the visit budget) */
+#define RT_FLAG_NO_FOLD      0x40u /* RT_TRAV_STATIC without exact constant folding of primitive tests */
 
 /* traversal policies (rt_stats.traversal) */
 #define RT_TRAV_LANE   0   /* per-lane DFS over an LDS stack (any scene) */
@@ -112,6 +113,8 @@ typedef struct rt_stats {
   int32_t traversal;       /* RT_TRAV_* used by the last render */
   int32_t jit_visits;      /* node visits of the specialised traversal (RT_TRAV_STATIC) */
   double sched_ms;         /* longest-first schedule: probe paths + tile sort, before the render kernel */
+  int32_t folded;          /* 1 if the specialised traversal used exactly folded primitive tests */
+  int32_t fold_rerenders;  /* frames re-rendered unfolded after a ray left the host's bound (expect 0) */
 } rt_stats;
 
 /* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of

@@ -225,3 +225,18 @@ def test_tile_schedules_agree(sched, monkeypatch):
     fb, _ = gpu(w.scene(), cam, p)
     rc, ref, _ = oracle_render(w.scene(), cam, p)
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 8, 13, 18, 19])
+def test_folded_and_unfolded_static_traversal(idx):
+    # exact constant folding of primitive tests (scene_codegen.cpp) must not change a single bit
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 48, 27)
+    p = rt.make_params(s, W, H, spp=4, bounces=min(s.max_bounces, 50), flags=rt.RT_FLAG_FORCE_STATIC)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    a, sa = gpu(w.scene(), cam, p)
+    p.flags = rt.RT_FLAG_FORCE_STATIC | rt.RT_FLAG_NO_FOLD
+    b, sb = gpu(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(a), bits(ref)) and np.array_equal(bits(b), bits(ref))
+    if sa.traversal == rt.RT_TRAV_STATIC:
+        assert sa.folded == 1 and sb.folded == 0 and sa.fold_rerenders == 0
