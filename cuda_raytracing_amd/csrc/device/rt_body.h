@@ -221,6 +221,14 @@ __device__ __forceinline__ void trav_reset(Trav &T, const Ray &r) {
   T.was_last = false; T.result = false;
 }
 
+// the same without 1/dir (scene-specialised traversal: computed lazily before box tests)
+__device__ __forceinline__ void trav_reset_dir(Trav &T) {
+  T.tmax = __builtin_huge_valf();
+  T.sp = 0;
+  T.tc = 0; T.yc = 0;
+  T.was_last = false; T.result = false;
+}
+
 // aabb_hit (:990-1025) with the cached 1/dir; the three early returns folded into one flag
 __device__ __forceinline__ bool box_hit(const Trav &T, const Ray &r, float x0, float x1, float y0, float y1,
                                         float z0, float z1) {
@@ -359,6 +367,24 @@ __device__ __forceinline__ void rotate_exit(Trav &T, Ray &r, Hit &h, float sn, f
   r.o = mk((cs * o.x) + (sn * o.z), o.y, (-sn * o.x) + (cs * o.z));
   r.d = mk((cs * d.x) + (sn * d.z), d.y, (-sn * d.x) + (cs * d.z));
   T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  if (T.was_last) {
+    const f3 p = h.p, n = h.n;
+    h.p = mk((cs * p.x) + (sn * p.z), p.y, (-sn * p.x) + (cs * p.z));
+    h.n = mk((cs * n.x) + (sn * n.z), n.y, (-sn * n.x) + (cs * n.z));
+  }
+}
+
+// y-rotation enter / cleanup without the 1/dir refresh (scene-specialised traversal)
+__device__ __forceinline__ void rotate_enter_dir(Trav &T, Ray &r, float sn, float cs) {
+  T.was_last = false;
+  const f3 o = r.o, d = r.d;
+  r.o = mk((cs * o.x) - (sn * o.z), o.y, (sn * o.x) + (cs * o.z));
+  r.d = mk((cs * d.x) - (sn * d.z), d.y, (sn * d.x) + (cs * d.z));
+}
+__device__ __forceinline__ void rotate_exit_dir(Trav &T, Ray &r, Hit &h, float sn, float cs) {
+  const f3 o = r.o, d = r.d;
+  r.o = mk((cs * o.x) + (sn * o.z), o.y, (-sn * o.x) + (cs * o.z));
+  r.d = mk((cs * d.x) + (sn * d.z), d.y, (-sn * d.x) + (cs * d.z));
   if (T.was_last) {
     const f3 p = h.p, n = h.n;
     h.p = mk((cs * p.x) + (sn * p.z), p.y, (-sn * p.x) + (cs * p.z));
@@ -551,6 +577,7 @@ template <int F, class Trace>
 __device__ __forceinline__ void render_body(const RenderArgs &A) {
   constexpr bool LDS = (F & kVarLds) != 0, COUNT = (F & kVarCount) != 0;
   constexpr bool NOISE = (F & kVarNoise) != 0, UV = (F & kVarUv) != 0;
+  constexpr bool TRACE = (F & kVarTrace) != 0;   // per-wave timeline into A.wave_trace (diagnostics)
   Mem<LDS> S{A.scene};
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
@@ -587,9 +614,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool exhausted = false;
   uint32_t tiles_taken = 0, rounds = 0;
   uint32_t probe_tile = 0, probe_rounds = 0;
-  uint64_t ph_refill = 0, ph_trace = 0, ph_shade = 0, t_mark = 0;   // wave-trace phase clocks
+  uint64_t ph_refill = 0, ph_trace = 0, ph_mat = 0, ph_shade = 0, t_mark = 0;   // wave-trace phase clocks
   uint64_t busy_lane_rounds = 0;
-  const uint64_t t_start = A.wave_trace ? __builtin_amdgcn_s_memrealtime() : 0;
+  const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
 
   auto camera_ray = [&]() {                                                 // :1561-1578
     const int32_t lr = pix / A.width, j = pix - lr * A.width;
@@ -621,7 +648,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   };
 
   for (;;) {
-    if (A.wave_trace) {
+    if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       if (t_mark) ph_shade += t - t_mark;
       t_mark = t;
@@ -685,7 +712,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     if (lanes == 0) break;   // queue exhausted and every lane idle
     rounds++;
     busy_lane_rounds += static_cast<uint64_t>(__popcll(lanes));
-    if (A.wave_trace) {
+    if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       ph_refill += t - t_mark;
       t_mark = t;
@@ -693,7 +720,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 
     // ---- trace one path segment per busy lane (hit(), :1340) ----
     Trace::template run<LDS, COUNT, UV>(S, A, busy, lanes, lane, stk, T, ray, h, vc);
-    if (A.wave_trace) {
+    if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       ph_trace += t - t_mark;
       t_mark = t;
@@ -795,7 +822,19 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       done = true;
       res = mk(A.bg[0], A.bg[1], A.bg[2]);
     }
+    if (TRACE) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph_mat += t - t_mark;
+      t_mark = t;
+    }
     if (done) {
+      // res = att_k * res + 0.0f from the deepest level (:1362-1368).  With res = (+-0,+-0,+-0) and
+      // finite attenuations every level yields +0, so such paths (absorbed, depth-exhausted, escaped
+      // into a black background) skip the stack reads; depth 0 keeps res itself
+      if (A.black_skip && depth > 0 && res.x == 0.0f && res.y == 0.0f && res.z == 0.0f) {
+        res = mk(0.0f, 0.0f, 0.0f);
+        depth = 0;
+      }
       for (int32_t k = static_cast<int32_t>(depth) - 1; k >= 0; --k) {      // :1362-1368
         f3 at;
         if (static_cast<uint32_t>(k) < A.rc_lds_levels) {
@@ -825,14 +864,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
   }
 
-  if (A.wave_trace && lane == 0) {
+  if (TRACE && A.wave_trace && lane == 0) {
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
     const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
     const uint32_t xcc = __builtin_amdgcn_s_getreg(20 | (15 << 11));   // HW_REG_XCC_ID
     unsigned long long *w = A.wave_trace + kWaveTraceWords * static_cast<size_t>(blockIdx.x * kWavesPerBlock + wave);
     w[0] = t_start; w[1] = t_end; w[2] = tiles_taken; w[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
     w[4] = rounds; w[5] = busy_lane_rounds;
-    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade;
+    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade; w[9] = ph_mat;
   }
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};

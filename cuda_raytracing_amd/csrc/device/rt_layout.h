@@ -63,11 +63,12 @@ constexpr int kChunk = 64;         // pixel ids handed to a wave per work-queue 
 // render-kernel variants: scene staged in LDS, counters, Perlin noise textures, sphere u,v (image
 // textures with pixels), wave-packet traversal.  Specialising keeps unused texture code out of the
 // register allocation (the Perlin + double-sine path alone costs ~40 VGPRs).
-enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket = 16 };
+enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket = 16,
+             kVarTrace = 32 /* wave timeline diagnostics; scene-specialised kernels only */ };
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
-// refill / traversal / shading
-constexpr uint32_t kWaveTraceWords = 9;
+// refill / traversal / unwind+accumulate+next camera ray / material scatter
+constexpr uint32_t kWaveTraceWords = 10;
 
 // Resident 256-thread blocks per CU allowed by the VGPR budget: 512 VGPRs per lane per SIMD, one
 // wave of each block per SIMD.  The persistent grid must never exceed residency (a block that starts
@@ -111,6 +112,8 @@ struct RenderArgs {
                                   // a hashed RNG; adds each path's round count to probe_cost[tile]
   uint32_t reverse_tiles;         // no order array: 1 = hand tiles out bottom row first
   uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
+  uint32_t black_skip;            // every attenuation is finite (host-checked): a path ending in
+                                  // (0,0,0) unwinds to +0 without reading its colour stack
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

@@ -67,13 +67,38 @@ static_assert(rt::CNT_BOUNCES == RT_CNT_BOUNCES && rt::CNT_SHADES == RT_CNT_SHAD
 static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::K_GROUP == RTR_OBJ_GROUP, "kinds");
 
 constexpr int kLptMinSpp = 16;
-constexpr float kFoldRayBound = 1.0e6f;   // fold only when every ray provably stays below this
+constexpr float kFoldRayBound = 1.0e6f;
+constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
+constexpr uint32_t kRcLdsMaxLevels = 16;   // fold only when every ray provably stays below this
 
 // Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
 // precondition, scene_codegen.cpp).  Primary rays: camera centre + lens offset, directions to the
 // viewport.  Secondary rays start on a primitive, inside the root BVH box, and leave in a direction
 // of length <= 2 + fuzz (Lambertian n + unit, metal unit + fuzz*unit, dielectric reflect/refract of
 // unit vectors).  Returns +inf when no bound is available (root is not a BVH node).
+// Every attenuation a material can return is finite: solid texture colours, metal albedos and image
+// texels are finite (Perlin noise and dielectrics are finite by construction).  Enables the black-path
+// unwind skip (RenderArgs::black_skip).
+bool attenuations_finite(const rt::SceneImage &img) {
+  auto fin = [&](uint32_t word) {
+    float x;
+    std::memcpy(&x, &img.words[word], 4);
+    return std::isfinite(x);
+  };
+  for (uint32_t m = 0; m < img.mat_count; ++m) {
+    const uint32_t b = img.off_mats + m * rt::kMatWords;
+    if (img.words[b + rt::M_KIND] == rt::MAT_METAL)
+      for (int k = 0; k < 3; ++k) if (!fin(b + rt::M_ALBEDO + k)) return false;
+  }
+  for (uint32_t t = 0; t < img.tex_count; ++t) {
+    const uint32_t b = img.off_texs + t * rt::kTexWords;
+    if (img.words[b + rt::T_KIND] == rt::T_SOLID)
+      for (int k = 0; k < 3; ++k) if (!fin(b + rt::T_RGB + k)) return false;
+  }
+  for (size_t w = img.off_pixels; w < img.words.size(); ++w) if (!fin(static_cast<uint32_t>(w))) return false;
+  return true;
+}
+
 float ray_bound(const rt::SceneImage &img, const rt_camera *cam, const rt_params *p) {
   auto ab = [](float x) { return std::fabs(x); };
   const rtr_vec3 *c0 = &cam->center, *fu = &cam->defocus_u, *fv = &cam->defocus_v;
@@ -124,7 +149,9 @@ struct rt_context {
   size_t wave_trace_words = 0;
   int sched = 0;   // RT_SCHED: 0 auto (longest-first when spp >= kLptMinSpp), 1 row-major, 2 reversed, 3 longest-first
   int blocks_per_cu = 0;
-  uint32_t rc_lds_levels = rt::kRcLdsLevels;   // RT_RC_LDS_LEVELS
+  uint32_t rc_lds_levels = rt::kRcLdsLevels;   // RT_RC_LDS_LEVELS (minimum; more when LDS is free)
+  bool rc_lds_auto = true;                      // RT_RC_LDS_LEVELS given: exactly that many
+  bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
   bool fold_enabled = true;
@@ -193,12 +220,17 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_FOLD")) c->fold_enabled = e[0] != '0';
   if (const char *e = std::getenv("RT_PROBE"))
     c->probe_per_tile = static_cast<uint32_t>(std::min(64, std::max(1, std::atoi(e))));
-  if (const char *e = std::getenv("RT_RC_LDS_LEVELS")) c->rc_lds_levels = static_cast<uint32_t>(std::atoi(e));
+  if (const char *e = std::getenv("RT_RC_LDS_LEVELS")) {
+    c->rc_lds_levels = static_cast<uint32_t>(std::atoi(e));
+    c->rc_lds_auto = false;
+  }
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
   if (c->img.stack_need > 512) { delete c; return RT_ERR_STACK; }
+  c->black_skip = attenuations_finite(c->img);
+  if (const char *e = std::getenv("RT_BLACK_SKIP")) c->black_skip = c->black_skip && e[0] != '0';
   DeviceGuard g(device);
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_context_destroy(c); return RT_ERR_HIP; }
@@ -244,12 +276,13 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   // launch geometry: persistent grid = resident blocks per CU x CUs
   c->lds = c->img.words.size() <= rt::kLdsSceneMaxWords && !(p->flags & RT_FLAG_GLOBAL_SCENE);
   const uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
-  const uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
-  const uint32_t rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
-  const size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * c->img.stack_need * 64 * 2;
+  uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
+  uint32_t rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
+  size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * c->img.stack_need * 64 * 2;
   c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
+  const int trace_bit = c->wave_trace_path.empty() ? 0 : rt::kVarTrace;   // scene-specialised kernels only
   // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
   // at most jit_budget node visits (every catalog scene but the large random ones), else the per-lane
   // DFS.  The wave-packet DFS is kept as an explicit option (fastest on tiny all-sphere scenes).
@@ -266,7 +299,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     std::string why;
     const bool want_fold = c->fold_enabled && !(p->flags & RT_FLAG_NO_FOLD) &&
                            ray_bound(c->img, cam, p) <= kFoldRayBound;
-    if (rt::jit_kernels(c->img, c->variant, c->jit_budget, want_fold, &jk, &why)) {
+    if (rt::jit_kernels(c->img, c->variant | trace_bit, c->jit_budget, want_fold, &jk, &why)) {
       c->used_fold = jk.folded;
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
@@ -278,10 +311,32 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     }
   }
   if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
-  if (jit_fn) c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4;   // straight-line: no stacks
+  if (jit_fn) {   // straight-line traversal: no stacks
+    stack_bytes = 0;
+    c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4;
+  }
   c->used_traversal = trav;
-  const int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes)
-                            : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
+  int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes) : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
+  if (c->rc_lds_auto) {
+    // give the colour stack every LDS byte the resident blocks leave unused (deeper paths then never
+    // touch HBM), without lowering residency
+    const size_t per_block = kLdsPerCu / static_cast<size_t>(std::max(per_cu, 1));
+    const size_t fixed = static_cast<size_t>(scene_lds_words) * 4 + stack_bytes;
+    const size_t level_bytes = static_cast<size_t>(rt::kWavesPerBlock) * 3 * 64 * 4;
+    if (per_block > fixed) {
+      const uint32_t fit = static_cast<uint32_t>((per_block - fixed) / level_bytes);
+      const uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
+      if (lv > rc_levels) {
+        const size_t lds2 = fixed + lv * level_bytes;
+        const int per_cu2 = jit_fn ? rt::jit_blocks_per_cu(jit_fn, lds2) : rt::render_blocks_per_cu(c->variant, lds2);
+        if (per_cu2 >= per_cu) {
+          rc_levels = lv;
+          rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
+          c->lds_bytes = lds2;
+        }
+      }
+    }
+  }
   uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
                     static_cast<uint64_t>(c->cu_count);
   const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
@@ -333,6 +388,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.probe_cost = nullptr;
   a.reverse_tiles = c->sched == 2 ? 1u : 0u;
   a.fold_violation = static_cast<uint32_t *>(c->work.p) + 15;   // zeroed with the work counters
+  a.black_skip = c->black_skip ? 1u : 0u;
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;

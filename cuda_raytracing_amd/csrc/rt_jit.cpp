@@ -63,7 +63,7 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
                 bool *folded) {
   std::string trace;
   if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
-  const int v = variant & (kVarLds | kVarNoise | kVarUv);
+  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace);
   *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
          "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render(RenderArgs A) {\n"
          "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"

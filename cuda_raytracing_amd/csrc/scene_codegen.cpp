@@ -34,6 +34,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "gpu_scene.h"
 
@@ -56,6 +57,20 @@ struct Gen {
   int indent = 4;
   bool ok = true;
   uint32_t uid = 0;
+  // lazy 1/dir: the reference recomputes 1/dir in every aabb_hit from the current ray; the kernels
+  // cache it in T.inv.  Here it is (re)computed only before a box test that follows a direction change
+  // (start, y-rotation enter/exit), instead of at every rotation — same values, fewer divisions.
+  bool inv_fresh = false;
+  std::vector<uint32_t> boxes_after;   // boxes_after[k]: BVH visits after pre-order visit k (pass 1)
+  std::vector<uint8_t> kinds;          // pass 1: kind of pre-order visit k (1-based)
+  bool collect = false;
+
+  void need_inv() {
+    if (inv_fresh) return;
+    line("T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);");
+    inv_fresh = true;
+  }
+  bool boxes_later() const { return visits < boxes_after.size() && boxes_after[visits] > 0; }
 
   static bool is_zero(uint32_t b) { return (b & 0x7fffffffu) == 0; }
   // c * x (x a runtime value, finite in folded code)
@@ -164,15 +179,21 @@ struct Gen {
     if (!ok) return;
     if (++visits > budget || depth > 256 || i >= img.node_count) { ok = false; return; }
     const uint32_t *w = node(i);
+    if (collect) {
+      if (kinds.size() <= visits) kinds.resize(visits + 1, 0);
+      kinds[visits] = static_cast<uint8_t>(w[W_KIND]);
+    }
     const std::string xf = (in_t || in_r) ? "true" : "false";
     switch (w[W_KIND]) {
       case K_BVH:
         line("if (COUNT) vc.k[" + u(K_BVH) + "]++;");
+        need_inv();
         line("if (box_hit(T, r, " + f(w[W_BOX]) + ", " + f(w[W_BOX + 1]) + ", " + f(w[W_BOX + 2]) + ", " +
              f(w[W_BOX + 3]) + ", " + f(w[W_BOX + 4]) + ", " + f(w[W_BOX + 5]) + ")) {   // node " + u(i));
         indent += 2;
         walk(w[W_AUX] & 0xffffu, in_t, in_r, depth + 1);
         walk(w[W_AUX] >> 16, in_t, in_r, depth + 1);
+        if (!inv_fresh && boxes_later()) need_inv();   // leave the block with a valid 1/dir
         indent -= 2;
         line("}");
         break;
@@ -216,10 +237,12 @@ struct Gen {
       case K_YROTATE:
         if (in_r) { ok = false; return; }
         line("if (COUNT) vc.k[" + u(K_YROTATE) + "]++;");
-        line("rotate_enter(T, r, " + f(w[W_SIN]) + ", " + f(w[W_COS]) + ");   // node " + u(i));
+        line("rotate_enter_dir(T, r, " + f(w[W_SIN]) + ", " + f(w[W_COS]) + ");   // node " + u(i));
+        inv_fresh = false;
         walk(w[W_AUX], in_t, true, depth + 1);
         line("if (COUNT) vc.k[" + u(K_YROTATE) + "]++;");
-        line("rotate_exit(T, r, h, " + f(w[W_SIN]) + ", " + f(w[W_COS]) + ");");
+        line("rotate_exit_dir(T, r, h, " + f(w[W_SIN]) + ", " + f(w[W_COS]) + ");");
+        inv_fresh = false;
         break;
       case K_GROUP:
         line("if (COUNT) vc.k[" + u(K_GROUP) + "]++;");
@@ -259,7 +282,17 @@ bool foldable(const SceneImage &img) {
 bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
                            bool *folded) {
   fold = fold && foldable(img);
+  Gen g1{img, max_visits};   // pass 1: pre-order visit kinds (for the lazy 1/dir)
+  g1.collect = true;
+  g1.walk(img.root, false, false, 0);
+  if (!g1.ok) {
+    if (visits) *visits = g1.visits;
+    return false;
+  }
   Gen g{img, max_visits};
+  g.boxes_after.assign(g1.kinds.size() + 1, 0);
+  for (size_t k = g1.kinds.size(); k-- > 0;)
+    g.boxes_after[k] = g.boxes_after[k + 1] + (k + 1 < g1.kinds.size() && g1.kinds[k + 1] == K_BVH ? 1u : 0u);
   g.fold = fold;
   g.fold_uv = fold && !img.needs_uv;
   g.walk(img.root, false, false, 0);
@@ -272,7 +305,7 @@ bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold
   *src += "  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &A, bool busy, uint64_t,\n";
   *src += "                                             uint32_t, uint16_t *, Trav &T, Ray &r, Hit &h, Visits &vc) {\n";
   *src += "    if (!busy) return;\n";
-  *src += "    trav_reset(T, r);\n";
+  *src += "    trav_reset_dir(T);\n";
   if (fold) {
     // the host enables folding only when it can bound every ray by 1e6 (camera + scene box + materials);
     // a lane that ever sees a larger or non-finite ray flags the frame, which the host then re-renders
