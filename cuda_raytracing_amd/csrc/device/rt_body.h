@@ -751,9 +751,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         // the division run once, after the loop, instead of on every try of every lane.
         const float s2 = x * x + y * y + z * z;
         bool acc = s2 > 0.0f && s2 <= 0.99999904632568359375f;           // 1 - 2^-20
-        if (!acc && s2 > 0.99999904632568359375f && s2 < 1.00000095367431640625f) {
+        const bool near1 = s2 > 0.99999904632568359375f && s2 < 1.00000095367431640625f;
+        if (__ballot(near1) != 0) {   // wave-uniform branch: keeps the rare exact test out of the loop
+          asm volatile("" ::: "memory");   // not speculated (the compiler would if-convert the sqrt)
           const float l = sqrtf(s2);
-          acc = l * l <= 1.0f;
+          if (near1) acc = l * l <= 1.0f;
         }
         if (acc) { ruv = mk(x, y, z); break; }
       }
