@@ -2,18 +2,22 @@
 """bench.py — Msamples/s of the per-pixel render path on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scene 0] [--width 1920] [--height 1080]
-                    [--spp 512] [--bounces 16] [--no-cpu-baseline]
+                    [--spp 512] [--bounces 16] [--inflight 2] [--no-cpu-baseline]
 
-A "step" is one frame: RNG seeding kernel + render kernel (+ the RCCL row gather to rank 0 when N>1),
-with the scene already resident in HBM.  Default workload = BASELINE config 2: scene 0 (fv1) at
-1920x1080, spp 512, depth 16 on one GPU.  With N ranks (torch.distributed.run, one process per GPU,
-backend "nccl" = RCCL) the frame grows to ~N x the pixels at the same aspect and camera (weak scaling)
-and rows are interleaved across ranks.  Rank 0 prints ONE JSON line.
+A "step" is one frame: RNG seeding + longest-first schedule probe + render kernel (+ the RCCL row
+gather to rank 0 when N>1), with the scene already resident in HBM.  Default workload = BASELINE
+config 2: scene 0 (fv1) at 1920x1080, spp 512, depth 16 on one GPU.  With N ranks
+(torch.distributed.run, one process per GPU, backend "nccl" = RCCL) the frame grows to ~N x the
+pixels at the same aspect and camera (weak scaling) and rows are interleaved across ranks.  Up to
+--inflight frames are queued at once on separate streams (frames are independent; the next frame
+fills the SIMDs the previous frame's slowest pixels leave idle).  Rank 0 prints ONE JSON line.
 
-The printed value is samples of all ranks / max-over-ranks wall time of the K timed steps.
+The printed value is samples of all ranks x K frames / max-over-ranks wall time of the K timed steps.
 roofline: VALU-bound kernel; achieved = algorithmic FP32 ops per render launch (op model of
-SURVEY §8d evaluated on this workload's measured per-sample visit counts) / the render kernel's mean
-HIP-event duration.  cpu_baseline: the C oracle on this host's cores over a bounded row sample.
+SURVEY §8d evaluated on this workload's measured per-sample visit counts) / the render kernel's
+HIP-event duration on an isolated frame (no overlap; profile with --inflight 1 to compare with
+rocprofv3).  cpu_baseline: the C oracle on this host's cores over a bounded row sample, whose GPU
+render is compared bit for bit.
 """
 from __future__ import annotations
 
@@ -137,6 +141,7 @@ def main():
     ap.add_argument("--bounces", type=int, default=16)
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle wall time (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2, help="frames queued at once (own context + stream each)")
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,9 +160,12 @@ def main():
     off, stride, rows = rt.shard_rows(H, rank, world_size)
     params = rt.make_params(settings, W, H, spp=args.spp, bounces=args.bounces,
                             row_offset=off, row_stride=stride, row_count=rows)
-    ctx = rt.RenderContext(world.scene(), device=local_rank)
-    stream = torch.cuda.current_stream()
-    out = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
+    nf = max(1, args.inflight)
+    ctxs = [rt.RenderContext(world.scene(), device=local_rank) for _ in range(nf)]
+    ctx = ctxs[0]
+    streams = [torch.cuda.Stream() for _ in range(nf)]
+    outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nf)]
+    stream, out = streams[0], outs[0]
     workload = f"scene{args.scene}_{rt.scene_name(args.scene)}_{W}x{H}_spp{args.spp}_d{args.bounces}"
 
     # ---- op model: per-sample event rates of THIS workload (counting variant, untimed) ----
@@ -169,25 +177,44 @@ def main():
     counters = cst.counter_dict()
     ops_per_sample = op_model(counters, counters["samples"])
 
-    def step():
-        ctx.render_into(cam, params, out.data_ptr(), stream.cuda_stream)
-        st = ctx.timing()                                     # waits on the frame's events
-        if world_size > 1:
-            gather_rows(out, H, W, rank, world_size)
-        return st
+    # Frames are independent, so up to `inflight` frames are queued on their own streams (each with its
+    # own context: RNG states, colour stack, schedule): the next frame's blocks fill the SIMDs that
+    # the previous frame's last pixels leave idle, and the rank-0 gather of frame k overlaps frame k+1.
+    # Every frame is rendered completely; the timed region ends when the last one is retired.
+    pending = []
+    stats = []
 
-    for _ in range(args.warmup):
-        step()
+    def launch(k):
+        i = k % nf
+        ctxs[i].render_into(cam, params, outs[i].data_ptr(), streams[i].cuda_stream)
+        pending.append(i)
+
+    def retire():
+        i = pending.pop(0)
+        st = ctxs[i].timing()                                  # waits on that frame's events
+        if world_size > 1:
+            gather_rows(outs[i], H, W, rank, world_size)
+        stats.append(st)
+
+    def run(frames):
+        for k in range(frames):
+            if len(pending) == nf:
+                retire()
+            launch(k)
+        while pending:
+            retire()
+
+    run(max(args.warmup, 1) if nf > 1 else args.warmup)
+    # one isolated frame: the render kernel's own duration for the roofline (no overlap)
+    launch(0)
+    retire()
+    iso = stats[-1]
+    stats.clear()
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    render_ms, init_ms, sched_ms = [], [], []
-    for _ in range(args.steps):
-        st = step()
-        render_ms.append(st.render_ms)
-        init_ms.append(st.init_ms)
-        sched_ms.append(st.sched_ms)
+    run(args.steps)
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -196,10 +223,13 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    render_ms = [st.render_ms for st in stats]
+    init_ms = [st.init_ms for st in stats]
+    sched_ms = [st.sched_ms for st in stats]
 
     samples_per_step = W * H * args.spp                  # all ranks together
     value = samples_per_step * args.steps / elapsed / 1e6
-    mean_render_ms = sum(render_ms) / len(render_ms)
+    mean_render_ms = iso.render_ms
     local_samples = rows * W * args.spp
     achieved = ops_per_sample * local_samples / (mean_render_ms / 1e3) / 1e12
 
@@ -222,11 +252,15 @@ def main():
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "parallelism": f"rows interleaved x{world_size}" + (" + RCCL gather" if world_size > 1 else ""),
                 "pixels_per_gpu": rows * W,
+                "frames_in_flight": nf,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
                 "kernel": "rt_static_render (hipRTC)" if cst.traversal == rt.RT_TRAV_STATIC else "render_kernel",
             },
-            "kernel_ms": {"render_mean": round(mean_render_ms, 3), "seed_mean": round(sum(init_ms) / len(init_ms), 3),
-                          "schedule_mean": round(sum(sched_ms) / len(sched_ms), 3)},
+            "kernel_ms": {"render_isolated": round(iso.render_ms, 3), "seed_isolated": round(iso.init_ms, 3),
+                          "schedule_isolated": round(iso.sched_ms, 3),
+                          "single_frame_msamples_s": round(local_samples / ((iso.render_ms + iso.init_ms +
+                                                                             iso.sched_ms) / 1e3) / 1e6, 1),
+                          "render_mean_in_flight": round(sum(render_ms) / len(render_ms), 3)},
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved, 3),
@@ -235,6 +269,7 @@ def main():
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": load_traffic(workload),
                 "ops_per_sample": round(ops_per_sample, 1),
+                "measured_on": "isolated frame: render-kernel HIP events on its stream",
                 "counters_per_sample": {k: round(v / max(counters["samples"], 1), 4) for k, v in counters.items()
                                         if k not in ("samples", "max_stack", "stack_overflow", "rng_draws")},
             },
@@ -246,7 +281,8 @@ def main():
             except Exception as e:  # the baseline must never hide the GPU number
                 line["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world_size > 1:
         dist.destroy_process_group()
 

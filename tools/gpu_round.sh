@@ -19,7 +19,7 @@ fi
 step bench 900 python3 bench.py ${BENCH_ARGS:-}
 if [ "${PROFILE:-1}" = 1 ]; then
   export TMPDIR=/tmp
-  step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+  step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline
 fi
 if [ "${PMC:-0}" = 1 ]; then
   step pmc 1000 python3 tools/profile_pmc.py --out "$PWD/gpurun_out/pmc" ${PMC_ARGS:---scene 0 --spp 512}
