@@ -201,7 +201,12 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
 // traversal state and the per-node operations of hit() (raytracing.cu:1079-1251)
 // ---------------------------------------------------------------------------------------------
 struct Ray { f3 o, d; float time; };
-struct Hit { f3 p, n; float t, u, v; uint32_t mat; bool front; };
+// n is the OUTWARD normal and fd = dot(dir, n) at hit time; the face test (fd < 0) and the flip of
+// hit_record_set_face_normal (:983-987) are applied when shading (hit_normal) — exact, because the
+// y-rotation cleanup that may transform n in between is linear and odd (R(-n) == -R(n) bitwise)
+struct Hit { f3 p, n; float t, u, v, fd; uint32_t mat; };
+__device__ __forceinline__ bool hit_front(const Hit &h) { return h.fd < 0.0f; }
+__device__ __forceinline__ f3 hit_normal(const Hit &h) { return hit_front(h) ? h.n : flip(h.n); }
 struct Visits { uint32_t k[7]; uint32_t max_sp; };
 
 // locals of hit() (:1082-1088) plus a cached 1/dir
@@ -210,7 +215,8 @@ struct Trav {
   float tmax;      // shrinking ray_tmax (closest hit so far)
   int sp;          // per-lane hit-stack depth (0 = traversal finished)
   int tc, yc;      // translation / y-rotation cleanup counters
-  bool was_last, result;
+  uint32_t was_last;   // 0/1 in a VGPR (a bool becomes per-join SALU lane-mask merges)
+  bool result;
 };
 
 __device__ __forceinline__ void trav_reset(Trav &T, const Ray &r) {
@@ -218,7 +224,7 @@ __device__ __forceinline__ void trav_reset(Trav &T, const Ray &r) {
   T.tmax = __builtin_huge_valf();
   T.sp = 0;
   T.tc = 0; T.yc = 0;
-  T.was_last = false; T.result = false;
+  T.was_last = 0; T.result = false;
 }
 
 // the same without 1/dir (scene-specialised traversal: computed lazily before box tests)
@@ -226,7 +232,7 @@ __device__ __forceinline__ void trav_reset_dir(Trav &T) {
   T.tmax = __builtin_huge_valf();
   T.sp = 0;
   T.tc = 0; T.yc = 0;
-  T.was_last = false; T.result = false;
+  T.was_last = 0; T.result = false;
 }
 
 // aabb_hit (:990-1025) with the cached 1/dir; the three early returns folded into one flag
@@ -265,11 +271,11 @@ __device__ __forceinline__ void planar_hit(Trav &T, const Ray &r, Hit &h, bool t
       if (tri) inside = inside & (alpha + beta <= 1.0f);
       if (inside) {
         h.u = alpha; h.v = beta; h.t = t; h.p = p; h.mat = mat;
-        h.front = dot(r.d, n) < 0;
-        h.n = h.front ? n : flip(n);
+        h.fd = dot(r.d, n);
+        h.n = n;
         T.tmax = t;
         T.result = true;
-        if (in_xf) T.was_last = true;
+        if (in_xf) T.was_last = 1;
       }
     }
   }
@@ -301,11 +307,11 @@ __device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32
         h.u = phi / (2 * pi);
         h.v = theta / pi;
       }
-      h.front = dot(r.d, outward) < 0;
-      h.n = h.front ? outward : flip(outward);
+      h.fd = dot(r.d, outward);
+      h.n = outward;
       T.tmax = h.t;
       T.result = true;
-      if (in_xf) T.was_last = true;
+      if (in_xf) T.was_last = 1;
     }
   }
 }
@@ -335,18 +341,18 @@ __device__ __forceinline__ void sphere_hit_static(Trav &T, const Ray &r, Hit &h,
         h.u = phi / (2 * pi);
         h.v = theta / pi;
       }
-      h.front = dot(r.d, outward) < 0;
-      h.n = h.front ? outward : flip(outward);
+      h.fd = dot(r.d, outward);
+      h.n = outward;
       T.tmax = h.t;
       T.result = true;
-      if (in_xf) T.was_last = true;
+      if (in_xf) T.was_last = 1;
     }
   }
 }
 
 // translation enter / cleanup (:1176-1191)
 __device__ __forceinline__ void translate_enter(Trav &T, Ray &r, f3 off) {
-  T.was_last = false;
+  T.was_last = 0;
   r.o = sub(r.o, off);
 }
 __device__ __forceinline__ void translate_exit(Trav &T, Ray &r, Hit &h, f3 off) {
@@ -356,7 +362,7 @@ __device__ __forceinline__ void translate_exit(Trav &T, Ray &r, Hit &h, f3 off) 
 
 // y-rotation enter / cleanup (:1192-1237): the ray is rotated in place and back (ulp drift kept)
 __device__ __forceinline__ void rotate_enter(Trav &T, Ray &r, float sn, float cs) {
-  T.was_last = false;
+  T.was_last = 0;
   const f3 o = r.o, d = r.d;
   r.o = mk((cs * o.x) - (sn * o.z), o.y, (sn * o.x) + (cs * o.z));
   r.d = mk((cs * d.x) - (sn * d.z), d.y, (sn * d.x) + (cs * d.z));
@@ -376,7 +382,7 @@ __device__ __forceinline__ void rotate_exit(Trav &T, Ray &r, Hit &h, float sn, f
 
 // y-rotation enter / cleanup without the 1/dir refresh (scene-specialised traversal)
 __device__ __forceinline__ void rotate_enter_dir(Trav &T, Ray &r, float sn, float cs) {
-  T.was_last = false;
+  T.was_last = 0;
   const f3 o = r.o, d = r.d;
   r.o = mk((cs * o.x) - (sn * o.z), o.y, (sn * o.x) + (cs * o.z));
   r.d = mk((cs * d.x) - (sn * d.z), d.y, (sn * d.x) + (cs * d.z));
@@ -604,9 +610,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
   f3 sum = mk(0, 0, 0);
   Trav T;
-  T.inv = mk(0, 0, 0); T.tmax = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = false; T.result = false;
+  T.inv = mk(0, 0, 0); T.tmax = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = 0; T.result = false;
   Hit h;
-  h.u = 0; h.v = 0; h.t = 0; h.mat = 0; h.front = false; h.p = mk(0, 0, 0); h.n = mk(0, 0, 0);
+  h.u = 0; h.v = 0; h.t = 0; h.fd = 0; h.mat = 0; h.p = mk(0, 0, 0); h.n = mk(0, 0, 0);
   Visits vc{};
   uint32_t c_bounce = 0, c_shade = 0, c_perlin = 0, c_samples = 0;
 
@@ -762,23 +768,25 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       ruv = scale(1.0f / length(ruv), ruv);
       bool scattered = false;
       f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
+      const bool hfront = hit_front(h);
+      const f3 hn = hfront ? h.n : flip(h.n);
       if (mkind == MAT_LAMBERTIAN) {                                        // :458-465
         scattered = true;
-        dir = add(h.n, ruv);
+        dir = add(hn, ruv);
         const float eps = 1e-8f;
-        if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = h.n;
+        if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = hn;
         att = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
       } else if (mkind == MAT_METAL) {                                      // :466-472
-        f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, h.n), h.n));
+        f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, hn), hn));
         dir = add(unit(rd), scale(asf(m1.y), ruv));
         att = mk(asf(m0.z), asf(m0.w), asf(m1.x));
-        scattered = dot(dir, h.n) > 0;
+        scattered = dot(dir, hn) > 0;
       } else if (mkind == MAT_DIELECTRIC) {                                 // :473-487
         att = mk(1.0f, 1.0f, 1.0f);
         const float ior = asf(m1.z);
-        const float ri = h.front ? (1.0f / ior) : ior;
+        const float ri = hfront ? (1.0f / ior) : ior;
         const f3 ud = unit(ray.d);
-        const float cos_t = fminf(dot(flip(ud), h.n), 1.0f);
+        const float cos_t = fminf(dot(flip(ud), hn), 1.0f);
         const float sin_t = sqrtf(1.0f - cos_t * cos_t);
         bool reflect_it = ri * sin_t > 1.0f;
         if (!reflect_it) {
@@ -787,12 +795,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           reflect_it = (r0 + (1.0f - r0) * rt_pow5f(1.0f - cos_t)) > random_test;
         }
         if (reflect_it) {
-          dir = sub(ud, scale(2.0f * dot(ud, h.n), h.n));
+          dir = sub(ud, scale(2.0f * dot(ud, hn), hn));
         } else {                                                            // refract (:416-422)
-          float ct = fminf(dot(flip(ud), h.n), 1.0f);
-          f3 perp = scale(ri, add(ud, scale(ct, h.n)));
+          float ct = fminf(dot(flip(ud), hn), 1.0f);
+          f3 perp = scale(ri, add(ud, scale(ct, hn)));
           float pl = length(perp);
-          f3 par = scale(-sqrtf(fabsf(1.0f - pl * pl)), h.n);
+          f3 par = scale(-sqrtf(fabsf(1.0f - pl * pl)), hn);
           dir = add(perp, par);
         }
         scattered = true;

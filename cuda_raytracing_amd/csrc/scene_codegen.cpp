@@ -145,12 +145,9 @@ struct Gen {
     if (tri) in += " & (al" + k + " + be" + k + " <= 1.0f)";
     line("if (" + in + ") {");
     indent += 2;
-    const uint32_t *n = w + W_NORMAL;
     line("h.u = al" + k + "; h.v = be" + k + "; h.t = t" + k + "; h.p = p" + k + "; h.mat = " + u(w[W_AUX]) + ";");
-    line("h.front = den" + k + " < 0.0f;");
-    line("h.n = h.front ? " + v3(w, W_NORMAL) + " : mk(" + f(n[0] ^ 0x80000000u) + ", " + f(n[1] ^ 0x80000000u) + ", " +
-         f(n[2] ^ 0x80000000u) + ");");
-    line(std::string("T.tmax = t") + k + "; T.result = true;" + (in_xf ? " T.was_last = true;" : ""));
+    line("h.fd = den" + k + "; h.n = " + v3(w, W_NORMAL) + ";   // dot(dir, n) == denom bitwise (same products)");
+    line(std::string("T.tmax = t") + k + ";" + (in_xf ? " T.was_last = 1;" : ""));
     indent -= 2;
     line("}");
     indent -= 2;
@@ -316,6 +313,9 @@ bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold
     *src += "    if (!small) atomicOr(A.fold_violation, 1u);\n";
   }
   *src += g.out;
+  // every accepted hit has a finite t (planar: |denom| >= 1e-8, finite numerator; sphere: root < tmax),
+  // so "some hit" is exactly "tmax left +inf" — no per-hit flag to merge across the nested ifs
+  *src += "    T.result = T.tmax != __builtin_huge_valf();\n";
   *src += "  }\n};\n";
   return true;
 }
