@@ -238,18 +238,21 @@ __device__ __forceinline__ void trav_reset_dir(Trav &T) {
 // aabb_hit (:990-1025) with the cached 1/dir; the three early returns folded into one flag
 __device__ __forceinline__ bool box_hit(const Trav &T, const Ray &r, float x0, float x1, float y0, float y1,
                                         float z0, float z1) {
+  // t0 starts at tmin > 0 and MAX(t0, x) = (t0 < x) ? x : t0 never lets a NaN in, so t0 stays a
+  // positive non-NaN and the ternary equals fmaxf (v_max_f32).  t1 keeps the ternary MIN: a NaN
+  // slab value does replace it (utility.h:6).
   float t0 = kTmin, t1 = T.tmax;
   float a = (x0 - r.o.x) * T.inv.x, c = (x1 - r.o.x) * T.inv.x;
   if (T.inv.x < 0.0f && a > c) { float s = a; a = c; c = s; }
-  t0 = tmax_(t0, a); t1 = tmin_(t1, c);
+  t0 = fmaxf(t0, a); t1 = tmin_(t1, c);
   bool miss = t1 <= t0;
   a = (y0 - r.o.y) * T.inv.y; c = (y1 - r.o.y) * T.inv.y;
   if (T.inv.y < 0.0f && a > c) { float s = a; a = c; c = s; }
-  t0 = tmax_(t0, a); t1 = tmin_(t1, c);
+  t0 = fmaxf(t0, a); t1 = tmin_(t1, c);
   miss |= t1 <= t0;
   a = (z0 - r.o.z) * T.inv.z; c = (z1 - r.o.z) * T.inv.z;
   if (T.inv.z < 0.0f && a > c) { float s = a; a = c; c = s; }
-  t0 = tmax_(t0, a); t1 = tmin_(t1, c);
+  t0 = fmaxf(t0, a); t1 = tmin_(t1, c);
   miss |= t1 <= t0;
   return !miss;
 }
@@ -624,12 +627,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   uint64_t busy_lane_rounds = 0;
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
 
-  auto camera_ray = [&]() {                                                 // :1561-1578
+  f3 pp = mk(0, 0, 0);   // the pixel's viewport point (:1565-1567), computed once per pixel
+  uint32_t pending = 0;   // 1: the lane's rejection sampling continues next round (A.max_tries)
+  float random_test = 0.0f;
+  const uint32_t try_cap = A.max_tries ? A.max_tries : 0xffffffffu;
+  auto pixel_point = [&]() {
     const int32_t lr = pix / A.width, j = pix - lr * A.width;
     const int32_t i = A.row_offset + lr * A.row_stride;
-    const f3 pp = add(mk(A.p00[0], A.p00[1], A.p00[2]),
-                      add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
-                          scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
+    pp = add(mk(A.p00[0], A.p00[1], A.p00[2]),
+             add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
+                 scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
+  };
+  auto camera_ray = [&]() {                                                 // :1561-1578
     if (A.defocus_angle <= 0) {
       ray.o = mk(A.center[0], A.center[1], A.center[2]);
     } else {                                                                // :1459-1476
@@ -708,6 +717,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           }
           sum = mk(0, 0, 0);
           sample = 0;
+          pixel_point();
           camera_ray();
         }
       }
@@ -725,7 +735,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
 
     // ---- trace one path segment per busy lane (hit(), :1340) ----
-    Trace::template run<LDS, COUNT, UV>(S, A, busy, lanes, lane, stk, T, ray, h, vc);
+    const bool tracing = busy && !pending;   // a lane still resuming its rejection keeps its hit
+    Trace::template run<LDS, COUNT, UV>(S, A, tracing, __ballot(tracing), lane, stk, T, ray, h, vc);
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       ph_trace += t - t_mark;
@@ -737,17 +748,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     // ---- shade (ray_color loop body, :1340-1359) ----
     bool done = false;
     f3 res = mk(0, 0, 0);
+    f3 ruv = mk(0, 0, 0);
     if (T.result) {
-      if (COUNT) c_shade++;
-      const uint32_t mbase = A.off_mats + h.mat * kMatWords;
-      const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
-      const uint32_t mkind = m0.x;
-      f3 emit = mk(0, 0, 0);
-      if (mkind == MAT_DIFFUSE_LIGHT) emit = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
-      // cuda_material_scatter: random_test first, then the unit vector (z, y, x) (:497-502, vec3.h:152-161)
-      const float random_test = rng.uniform();
-      f3 ruv;
-      for (;;) {
+      // cuda_material_scatter: random_test first, then the unit vector by rejection, drawn (z, y, x)
+      // (:497-502, vec3.h:152-161) — for every material, lights included.  With A.max_tries > 0 a lane
+      // whose tries all fail keeps its hit and resumes the rejection next round (skipping that round's
+      // traversal), so one unlucky lane no longer holds the whole wave in this loop.
+      if (!pending) {
+        if (COUNT) c_shade++;
+        random_test = rng.uniform();
+      }
+      bool got = false;
+      for (uint32_t k = 0; k != try_cap; ++k) {
         float z = rng.bound(-1.0f, 1.0f);
         float y = rng.bound(-1.0f, 1.0f);
         float x = rng.bound(-1.0f, 1.0f);
@@ -763,8 +775,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           const float l = sqrtf(s2);
           if (near1) acc = l * l <= 1.0f;
         }
-        if (acc) { ruv = mk(x, y, z); break; }
+        if (acc) { ruv = mk(x, y, z); got = true; break; }
       }
+      pending = got ? 0u : 1u;
+    }
+    if (T.result && !pending) {
+      const uint32_t mbase = A.off_mats + h.mat * kMatWords;
+      const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
+      const uint32_t mkind = m0.x;
+      f3 emit = mk(0, 0, 0);
+      if (mkind == MAT_DIFFUSE_LIGHT) emit = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
       ruv = scale(1.0f / length(ruv), ruv);
       bool scattered = false;
       f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
@@ -828,7 +848,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         done = true;
         res = emit;
       }
-    } else {
+    } else if (!T.result) {
       done = true;
       res = mk(A.bg[0], A.bg[1], A.bg[2]);
     }

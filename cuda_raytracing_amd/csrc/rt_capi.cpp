@@ -152,6 +152,7 @@ struct rt_context {
   uint32_t rc_lds_levels = rt::kRcLdsLevels;   // RT_RC_LDS_LEVELS (minimum; more when LDS is free)
   bool rc_lds_auto = true;                      // RT_RC_LDS_LEVELS given: exactly that many
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
+  uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
   bool fold_enabled = true;
@@ -225,6 +226,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->rc_lds_auto = false;
   }
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
+  if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
@@ -389,6 +391,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.reverse_tiles = c->sched == 2 ? 1u : 0u;
   a.fold_violation = static_cast<uint32_t *>(c->work.p) + 15;   // zeroed with the work counters
   a.black_skip = c->black_skip ? 1u : 0u;
+  a.max_tries = c->max_tries;
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;

@@ -64,8 +64,12 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
   std::string trace;
   if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
   const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace);
+  // RT_JIT_WAVES=N asks the register allocator for N waves per SIMD (A/B; default: unconstrained)
+  std::string attr;
+  if (const char *e = std::getenv("RT_JIT_WAVES"))
+    if (std::atoi(e) > 0) attr = " __attribute__((amdgpu_waves_per_eu(" + std::to_string(std::atoi(e)) + ")))";
   *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
-         "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render(RenderArgs A) {\n"
+         "extern \"C\" __global__ __launch_bounds__(256)" + attr + " void rt_static_render(RenderArgs A) {\n"
          "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render_count(RenderArgs A) {\n"
          "  render_body<" + std::to_string(v | kVarCount) + ", StaticTrace>(A);\n}\n"

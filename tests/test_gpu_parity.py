@@ -240,3 +240,18 @@ def test_folded_and_unfolded_static_traversal(idx):
     assert rc == 0 and np.array_equal(bits(a), bits(ref)) and np.array_equal(bits(b), bits(ref))
     if sa.traversal == rt.RT_TRAV_STATIC:
         assert sa.folded == 1 and sb.folded == 0 and sa.fold_rerenders == 0
+
+
+@pytest.mark.parametrize("tries", ["1", "2", "3"])
+@pytest.mark.parametrize("idx", [0, 1, 8])
+def test_capped_rejection_tries_agree(idx, tries, monkeypatch):
+    # deferring an unfinished rejection loop to the next round must not change any draw or result
+    monkeypatch.setenv("RT_MAX_TRIES", tries)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 33, 19)
+    for force in (rt.RT_FLAG_FORCE_STATIC, rt.RT_FLAG_FORCE_LANE):
+        p = rt.make_params(s, W, H, spp=5, bounces=min(s.max_bounces, 50), flags=force | rt.RT_FLAG_COUNT)
+        fb, st = gpu(w.scene(), cam, p)
+        rc, ref, ost = oracle_render(w.scene(), cam, p)
+        assert rc == 0 and np.array_equal(bits(fb), bits(ref)), (idx, tries, force)
+        assert st.counter_dict()["shades"] == ost.counter_dict()["shades"]
