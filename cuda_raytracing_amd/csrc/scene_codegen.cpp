@@ -65,6 +65,11 @@ struct Gen {
   std::vector<uint8_t> kinds;          // pass 1: kind of pre-order visit k (1-based)
   bool collect = false;
 
+  bool span1_primitive(const uint32_t *w) const {
+    if ((w[W_AUX] & 0xffffu) != (w[W_AUX] >> 16) || (w[W_AUX] & 0xffffu) >= img.node_count) return false;
+    const uint32_t ck = node(w[W_AUX] & 0xffffu)[W_KIND];
+    return ck == K_SPHERE || ck == K_QUAD || ck == K_TRIANGLE;
+  }
   void need_inv() {
     if (inv_fresh) return;
     line("T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);");
@@ -183,6 +188,23 @@ struct Gen {
     const std::string xf = (in_t || in_r) ? "true" : "false";
     switch (w[W_KIND]) {
       case K_BVH:
+        if (span1_primitive(w)) {
+          // span-1 leaf (both children the same sphere/quad/triangle, raytracing.cu:858-859): the second
+          // test can never change the record (a sphere re-test rejects root1 == tmax and root2 >= root1;
+          // a planar re-test rewrites identical values), so it is emitted once and counted twice
+          line("if (COUNT) vc.k[" + u(K_BVH) + "]++;");
+          need_inv();
+          line("if (box_hit(T, r, " + f(w[W_BOX]) + ", " + f(w[W_BOX + 1]) + ", " + f(w[W_BOX + 2]) + ", " +
+               f(w[W_BOX + 3]) + ", " + f(w[W_BOX + 4]) + ", " + f(w[W_BOX + 5]) + ")) {   // node " + u(i) +
+               " (span 1)");
+          indent += 2;
+          line("if (COUNT) vc.k[" + u(node(w[W_AUX] & 0xffffu)[W_KIND]) + "]++;");
+          walk(w[W_AUX] & 0xffffu, in_t, in_r, depth + 1);
+          if (!inv_fresh && boxes_later()) need_inv();
+          indent -= 2;
+          line("}");
+          break;
+        }
         line("if (COUNT) vc.k[" + u(K_BVH) + "]++;");
         need_inv();
         line("if (box_hit(T, r, " + f(w[W_BOX]) + ", " + f(w[W_BOX + 1]) + ", " + f(w[W_BOX + 2]) + ", " +
