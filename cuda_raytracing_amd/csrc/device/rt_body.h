@@ -405,7 +405,8 @@ __device__ __forceinline__ void rotate_exit_dir(Trav &T, Ray &r, Hit &h, float s
 // traversal policy 1: per-lane DFS with a lane-interleaved LDS stack (any scene)
 // ---------------------------------------------------------------------------------------------
 // One iteration of hit()'s while loop (:1089-1249): pop one record and process it.
-template <bool LDS, bool COUNT, bool UV>
+// KM: kinds that can occur in the scene (bit K_*); the run-time compiled lane kernels drop the others
+template <bool LDS, bool COUNT, bool UV, uint32_t KM = 0x7fu>
 __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hit &h, uint16_t *stk, Visits &vc) {
   int sp = T.sp - 1;
   const uint32_t idx = stk[sp * 64];
@@ -414,23 +415,23 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
   const uint32_t kind = w0.x;
   if (COUNT) { vc.k[kind < 7 ? kind : 0]++; }
   const bool in_xf = T.tc || T.yc;
-  if (kind == K_BVH) {                                                     // :1124-1130
+  if ((KM & (1u << K_BVH)) && kind == K_BVH) {                             // :1124-1130
     const uint4 w1 = S.w4(nb + 4);
     if (box_hit(T, r, asf(w0.z), asf(w0.w), asf(w1.x), asf(w1.y), asf(w1.z), asf(w1.w))) {
       stk[sp * 64] = static_cast<uint16_t>(w0.y >> 16);      // right
       stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);      // left (popped first)
       sp += 2;
     }
-  } else if (kind == K_QUAD || kind == K_TRIANGLE) {
+  } else if ((KM & ((1u << K_QUAD) | (1u << K_TRIANGLE))) && (kind == K_QUAD || kind == K_TRIANGLE)) {
     const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8), w3 = S.w4(nb + 12), w4 = S.w4(nb + 16);
     planar_hit(T, r, h, kind == K_TRIANGLE, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), asf(w1.y),
                mk(asf(w1.z), asf(w1.w), asf(w2.x)), mk(asf(w2.y), asf(w2.z), asf(w2.w)),
                mk(asf(w3.x), asf(w3.y), asf(w3.z)), mk(asf(w3.w), asf(w4.x), asf(w4.y)), in_xf);
-  } else if (kind == K_SPHERE) {
+  } else if ((KM & (1u << K_SPHERE)) && kind == K_SPHERE) {
     const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8);
     sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
                    asf(w2.y), asf(w2.z), in_xf);
-  } else if (kind == K_TRANSLATE) {
+  } else if ((KM & (1u << K_TRANSLATE)) && kind == K_TRANSLATE) {
     const uint4 w1 = S.w4(nb + 4);
     const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
     if (T.tc == 0) {
@@ -443,7 +444,7 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
       T.tc--;
       translate_exit(T, r, h, off);
     }
-  } else if (kind == K_YROTATE) {
+  } else if ((KM & (1u << K_YROTATE)) && kind == K_YROTATE) {
     if (T.yc == 0) {
       rotate_enter(T, r, asf(w0.z), asf(w0.w));
       stk[sp * 64] = static_cast<uint16_t>(idx);
@@ -454,7 +455,7 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
       T.yc--;
       rotate_exit(T, r, h, asf(w0.z), asf(w0.w));
     }
-  } else if (kind == K_GROUP) {                                           // :1238-1247
+  } else if ((KM & (1u << K_GROUP)) && kind == K_GROUP) {               // :1238-1247
     const uint32_t first = w0.y, n = w0.z;
     for (uint32_t i = 0; i < n; ++i) stk[(sp + i) * 64] = static_cast<uint16_t>(first + i);
     sp += n;
@@ -463,7 +464,8 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
   T.sp = sp;
 }
 
-struct LaneTrace {
+template <uint32_t KM>
+struct LaneTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t, uint32_t,
                                              uint16_t *stk, Trav &T, Ray &r, Hit &h, Visits &vc) {
@@ -471,9 +473,10 @@ struct LaneTrace {
     trav_reset(T, r);
     stk[0] = static_cast<uint16_t>(A.root);
     T.sp = 1;
-    while (T.sp > 0) trav_step<LDS, COUNT, UV>(S, T, r, h, stk, vc);
+    while (T.sp > 0) trav_step<LDS, COUNT, UV, KM>(S, T, r, h, stk, vc);
   }
 };
+using LaneTrace = LaneTraceK<0x7fu>;
 
 // ---------------------------------------------------------------------------------------------
 // traversal policy 2: one DFS per wave with per-entry lane masks

@@ -153,6 +153,7 @@ struct rt_context {
   bool rc_lds_auto = true;                      // RT_RC_LDS_LEVELS given: exactly that many
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
+  bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
   bool fold_enabled = true;
@@ -226,6 +227,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->rc_lds_auto = false;
   }
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
+  if (const char *e = std::getenv("RT_JIT_LANE")) c->lane_jit = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
@@ -295,6 +297,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC)) trav = RT_TRAV_LANE;
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
   hipFunction_t jit_fn = nullptr, jit_probe = nullptr;
+  bool jit_lane = false;
   c->used_fold = false;
   if (trav < 0 || trav == RT_TRAV_STATIC) {
     rt::JitKernels jk;
@@ -312,8 +315,21 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
       trav = RT_TRAV_LANE;
     }
   }
+  if (trav == RT_TRAV_LANE && c->lane_jit && !(p->flags & RT_FLAG_NO_JIT)) {
+    // per-lane DFS compiled for the node kinds this scene has (fewer branches and registers than
+    // the offline all-kinds kernel); the offline kernel stays the fallback
+    rt::JitKernels jk;
+    std::string why;
+    if (rt::jit_lane_kernels(c->img, c->variant | trace_bit, &jk, &why)) {
+      jit_fn = c->counted ? jk.render_count : jk.render;
+      jit_probe = jk.probe;
+      jit_lane = true;
+    } else if (c->jit_why.empty()) {
+      c->jit_why = why;
+    }
+  }
   if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
-  if (jit_fn) {   // straight-line traversal: no stacks
+  if (jit_fn && !jit_lane) {   // straight-line traversal: no stacks
     stack_bytes = 0;
     c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4;
   }

@@ -121,14 +121,10 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
   return ok;
 }
 
-bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
-  std::string src;
-  uint32_t visits = 0;
-  bool folded = false;
-  if (!jit_source(img, variant, max_visits, fold, &src, &visits, &folded)) {
-    if (why) *why = "scene expansion exceeds " + std::to_string(max_visits) + " node visits";
-    return false;
-  }
+namespace {
+
+// Compile (or fetch) the module of `src` exporting <prefix>_render, <prefix>_render_count, <prefix>_probe.
+bool build_module(const std::string &src, const std::string &prefix, JitKernels *out, std::string *why) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const std::string arch = arch_of(dev);
@@ -144,14 +140,12 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
     if (!jit_compile(src, arch, &code, &log)) {
       e->why = "hipRTC compile failed: " + log.substr(0, 2000);
     } else if (hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
-               hipModuleGetFunction(&e->k.render, e->mod, "rt_static_render") != hipSuccess ||
-               hipModuleGetFunction(&e->k.render_count, e->mod, "rt_static_render_count") != hipSuccess ||
-               hipModuleGetFunction(&e->k.probe, e->mod, "rt_static_probe") != hipSuccess) {
+               hipModuleGetFunction(&e->k.render, e->mod, (prefix + "_render").c_str()) != hipSuccess ||
+               hipModuleGetFunction(&e->k.render_count, e->mod, (prefix + "_render_count").c_str()) != hipSuccess ||
+               hipModuleGetFunction(&e->k.probe, e->mod, (prefix + "_probe").c_str()) != hipSuccess) {
       e->why = "hipModuleLoadData/GetFunction failed";
     } else {
       e->ok = true;
-      e->k.visits = visits;
-      e->k.folded = folded;
     }
     it = g_cache.emplace(key, std::move(e)).first;
   }
@@ -159,8 +153,56 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
     if (why) *why = it->second->why;
     return false;
   }
+  const uint32_t visits = out->visits;
+  const bool folded = out->folded;
   *out = it->second->k;
+  out->visits = visits;
+  out->folded = folded;
   return true;
+}
+
+}  // namespace
+
+bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
+  std::string src;
+  uint32_t visits = 0;
+  bool folded = false;
+  if (!jit_source(img, variant, max_visits, fold, &src, &visits, &folded)) {
+    if (why) *why = "scene expansion exceeds " + std::to_string(max_visits) + " node visits";
+    return false;
+  }
+  out->visits = visits;
+  out->folded = folded;
+  return build_module(src, "rt_static", out, why);
+}
+
+uint32_t scene_kinds(const SceneImage &img) {
+  uint32_t km = 0;
+  for (uint32_t i = 0; i < img.node_count; ++i) {
+    const uint32_t k = img.words[static_cast<size_t>(i) * kNodeWords + W_KIND];
+    if (k < 7) km |= 1u << k;
+  }
+  return km;
+}
+
+std::string jit_lane_source(const SceneImage &img, int variant) {
+  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace);
+  const std::string lt = "LaneTraceK<" + std::to_string(scene_kinds(img)) + "u>";
+  std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render(RenderArgs A) {\n  render_body<" +
+         std::to_string(v) + ", " + lt + ">(A);\n}\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render_count(RenderArgs A) {\n  render_body<" +
+         std::to_string(v | kVarCount) + ", " + lt + ">(A);\n}\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_probe(RenderArgs A) {\n  render_body<" +
+         std::to_string(v) + ", " + lt + ">(A);\n}\n";
+  src += "}  // namespace rt\n";
+  return src;
+}
+
+bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
+  out->visits = 0;
+  out->folded = false;
+  return build_module(jit_lane_source(img, variant), "rt_lane", out, why);
 }
 
 hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s) {

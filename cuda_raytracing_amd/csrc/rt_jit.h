@@ -29,6 +29,12 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
 // Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
 
+// Per-lane DFS kernels specialised on the node kinds present in the scene (large scenes: the
+// kind dispatch of trav_step keeps only those branches).  Same contract as jit_kernels.
+bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
+std::string jit_lane_source(const SceneImage &img, int variant);
+uint32_t scene_kinds(const SceneImage &img);
+
 // extra hipRTC options from the RT_JIT_OPTS environment variable (space separated)
 std::vector<std::string> jit_extra_options();
 

@@ -255,3 +255,17 @@ def test_capped_rejection_tries_agree(idx, tries, monkeypatch):
         rc, ref, ost = oracle_render(w.scene(), cam, p)
         assert rc == 0 and np.array_equal(bits(fb), bits(ref)), (idx, tries, force)
         assert st.counter_dict()["shades"] == ost.counter_dict()["shades"]
+
+
+@pytest.mark.parametrize("idx", [1, 2, 13, 17, 20])
+def test_offline_and_jit_lane_kernels_agree(idx):
+    # the offline all-kinds lane kernel (RT_FLAG_NO_JIT) and the kind-specialised hipRTC one
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 36, 20)
+    p = rt.make_params(s, W, H, spp=3, bounces=min(s.max_bounces, 50), flags=rt.RT_FLAG_FORCE_LANE | rt.RT_FLAG_COUNT)
+    a, sa = gpu(w.scene(), cam, p)
+    p.flags = rt.RT_FLAG_FORCE_LANE | rt.RT_FLAG_NO_JIT | rt.RT_FLAG_COUNT
+    b, sb = gpu(w.scene(), cam, p)
+    rc, ref, ost = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(a), bits(ref)) and np.array_equal(bits(b), bits(ref))
+    assert sa.counter_dict()["visit_bvh"] == sb.counter_dict()["visit_bvh"] == ost.counter_dict()["visit_bvh"]
