@@ -4,8 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scene 0] [--width 1920] [--height 1080]
                     [--spp 512] [--bounces 16] [--inflight 2] [--no-cpu-baseline]
 
-A "step" is one frame: RNG seeding + longest-first schedule probe + render kernel (+ the RCCL row
-gather to rank 0 when N>1), with the scene already resident in HBM.  Default workload = BASELINE
+A "step" is one frame: RNG seeding + longest-first schedule probe + render kernel + device tonemap
+to PPM bytes (+ the RCCL gather of the u8 rows to rank 0 when N>1), with the scene already resident
+in HBM.  Default workload = BASELINE
 config 2: scene 0 (fv1) at 1920x1080, spp 512, depth 16 on one GPU.  With N ranks
 (torch.distributed.run, one process per GPU, backend "nccl" = RCCL) the frame grows to ~N x the
 pixels at the same aspect and camera (weak scaling) and rows are interleaved across ranks.  Up to
@@ -165,6 +166,7 @@ def main():
     ctx = ctxs[0]
     streams = [torch.cuda.Stream() for _ in range(nf)]
     outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nf)]
+    outs8 = [torch.empty((rows, W, 3), dtype=torch.uint8, device="cuda") for _ in range(nf)]
     stream, out = streams[0], outs[0]
     workload = f"scene{args.scene}_{rt.scene_name(args.scene)}_{W}x{H}_spp{args.spp}_d{args.bounces}"
 
@@ -187,13 +189,15 @@ def main():
     def launch(k):
         i = k % nf
         ctxs[i].render_into(cam, params, outs[i].data_ptr(), streams[i].cuda_stream)
+        rt.tonemap_device(outs[i], outs8[i], streams[i].cuda_stream)   # PPM bytes on the device
         pending.append(i)
 
     def retire():
         i = pending.pop(0)
-        st = ctxs[i].timing()                                  # waits on that frame's events
+        st = ctxs[i].timing()                                  # waits on that frame's render events
+        torch.cuda.current_stream().wait_stream(streams[i])    # ... and its tonemap
         if world_size > 1:
-            gather_rows(outs[i], H, W, rank, world_size)
+            gather_rows(outs8[i], H, W, rank, world_size)      # u8 rows: 3 B/pixel over xGMI
         stats.append(st)
 
     def run(frames):
@@ -250,7 +254,8 @@ def main():
             "config": {
                 "workload": workload,
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
-                "parallelism": f"rows interleaved x{world_size}" + (" + RCCL gather" if world_size > 1 else ""),
+                "parallelism": f"rows interleaved x{world_size}" + (" + RCCL u8 gather" if world_size > 1 else ""),
+                "output": "PPM bytes on the device (rt_tonemap_device)",
                 "pixels_per_gpu": rows * W,
                 "frames_in_flight": nf,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),

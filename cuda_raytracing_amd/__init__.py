@@ -23,7 +23,7 @@ __all__ = [
     "camera_from_settings", "make_params", "render", "RenderContext", "tonemap", "write_ppm",
     "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE",
     "RT_FLAG_NO_JIT", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_TRAV_LANE",
-    "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
+    "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "tonemap_device", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError",
 ]
 
@@ -288,6 +288,18 @@ def tonemap(rgb: np.ndarray) -> np.ndarray:
     src = np.ascontiguousarray(rgb, dtype=np.float32)
     out = np.empty(src.shape, dtype=np.uint8)
     _abi.host_lib().rt_tonemap(src.ctypes.data_as(C.c_void_p), src.size // 3, out.ctypes.data_as(C.c_void_p))
+    return out
+
+
+def tonemap_device(rgb, out=None, stream: int = 0):
+    """GPU tonemap (rt_tonemap_device) of a float32 CUDA tensor [..., 3] -> uint8 tensor, same shape."""
+    import torch
+    if not (rgb.is_cuda and rgb.dtype == torch.float32 and rgb.is_contiguous()):
+        raise ValueError("tonemap_device expects a contiguous float32 device tensor")
+    if out is None:
+        out = torch.empty(rgb.shape, dtype=torch.uint8, device=rgb.device)
+    _check(_abi.hip_lib().rt_tonemap_device(C.c_void_p(rgb.data_ptr()), rgb.numel() // 3,
+                                            C.c_void_p(out.data_ptr()), C.c_void_p(stream)), "rt_tonemap_device")
     return out
 
 

@@ -162,7 +162,7 @@ def host_lib():
 
 HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_timing",
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
-               "rt_static_source", "rt_static_compile", "rt_context_note"]
+               "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device"]
 
 
 def _bind_single_hip_runtime():
@@ -203,6 +203,7 @@ def hip_lib():
         _sig(L.rt_static_compile, C.c_int, C.POINTER(Scene), C.c_uint32, C.c_char_p, C.c_char_p,
              C.c_uint64)
         _sig(L.rt_context_note, C.c_char_p, P)
+        _sig(L.rt_tonemap_device, C.c_int, P, C.c_uint64, P, P)
         _hip = L
     return _hip
 

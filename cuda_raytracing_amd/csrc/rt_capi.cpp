@@ -580,4 +580,10 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
   return ok ? RT_OK : RT_ERR_HIP;
 }
 
+int rt_tonemap_device(const float *rgb, uint64_t pixels, uint8_t *out, void *stream) {
+  if ((!rgb || !out) && pixels) return RT_ERR_INVALID_ARG;
+  if (rt::launch_tonemap(rgb, pixels * 3, out, static_cast<hipStream_t>(stream)) != hipSuccess) return RT_ERR_HIP;
+  return RT_OK;
+}
+
 const char *rt_context_note(const rt_context *c) { return c ? c->jit_why.c_str() : ""; }

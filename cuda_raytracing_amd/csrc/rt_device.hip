@@ -92,7 +92,34 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint32_t *co
   for (uint32_t i = t; i < n; i += kOrderThreads) order[atomicAdd(&hist[key(cost[i])], 1u)] = i;
 }
 
+// linear -> 8-bit sRGB-ish bytes of pixels_to_ppm (raytracing.cu:1391-1395,1419-1431): sqrt gamma
+// (0 for non-positive), clamp to [0, 0.999], (u8)(256 * x).  Each thread converts 4 consecutive
+// floats (16-B load, 4-B store); HBM-bound (12 B in, 3 B out per pixel).
+__global__ __launch_bounds__(256) void tonemap_kernel(const float *__restrict__ rgb, uint64_t n,
+                                                      uint8_t *__restrict__ out) {
+  const uint64_t i = (static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  auto byte = [](float c) -> uint32_t {
+    const float g = c > 0 ? sqrtf(c) : 0.0f;
+    const float k = (g < 0.0f) ? 0.0f : ((g > 0.999f) ? 0.999f : g);
+    return static_cast<uint32_t>(256 * k) & 0xffu;
+  };
+  if (i + 4 <= n && (reinterpret_cast<uintptr_t>(rgb + i) & 15) == 0 && (reinterpret_cast<uintptr_t>(out + i) & 3) == 0) {
+    const float4 v = *reinterpret_cast<const float4 *>(rgb + i);
+    *reinterpret_cast<uint32_t *>(out + i) = byte(v.x) | (byte(v.y) << 8) | (byte(v.z) << 16) | (byte(v.w) << 24);
+  } else {
+    for (uint64_t k = i; k < n && k < i + 4; ++k) out[k] = static_cast<uint8_t>(byte(rgb[k]));
+  }
+}
+
 }  // namespace
+
+hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + 1023) / 1024;
+  hipLaunchKernelGGL(tonemap_kernel, dim3(static_cast<uint32_t>(blocks)), dim3(256), 0, s, rgb, n, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s) {
   hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, s, cost, n, order);

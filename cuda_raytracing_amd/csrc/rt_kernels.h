@@ -11,6 +11,8 @@ constexpr uint32_t kLdsSceneMaxWords = 12 * 1024;   // stage scenes up to 48 KiB
 constexpr uint32_t kPacketMaxNodes = 512;           // packet DFS only for scenes up to this size
 
 hipError_t launch_seed(const SeedArgs &a, hipStream_t s);
+// pixels_to_ppm byte conversion of n floats (3 per pixel) on the device
+hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_t s);
 // longest-first order of n tiles from probe costs (single block)
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s);
 hipError_t launch_render(const RenderArgs &a, int variant, uint32_t blocks, size_t lds_bytes, hipStream_t s);

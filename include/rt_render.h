@@ -134,6 +134,12 @@ int rt_context_render(rt_context *ctx, const rt_camera *camera, const rt_params 
 int rt_context_timing(rt_context *ctx, rt_stats *stats);
 void rt_context_destroy(rt_context *ctx);
 
+/* Device tonemap: the byte conversion of pixels_to_ppm (raytracing.cu:1391-1395,
+ * 1419-1431) — sqrt gamma, clamp [0, 0.999], (u8)(256 x) — from a device framebuffer of `pixels`
+ * RGB float triples to 3*pixels device bytes (P6 payload order), asynchronously on `stream`.
+ * Bit-identical to the host conversion (rt_tonemap in rt_host.h). */
+int rt_tonemap_device(const float *rgb_device, uint64_t pixels, uint8_t *out_device, void *stream);
+
 /* Diagnostics for the scene-specialised traversal (no device needed).
  * rt_static_source: writes the hipRTC source for `scene` (NUL-terminated, truncated to cap) and the
  *   number of node visits of the expanded DFS; RT_ERR_UNSUPPORTED if it exceeds max_visits.

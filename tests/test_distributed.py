@@ -38,9 +38,12 @@ def _worker(rank, world, port, W, H, result):
                                                                  row_stride=stride, row_count=cnt))
     assert rc == 0
     img = gather_rows(torch.from_numpy(shard), H, W, rank, world)
+    # the u8 (PPM byte) gather the bench uses after the device tonemap: 4x smaller messages
+    img8 = gather_rows(torch.from_numpy(rt.tonemap(shard)), H, W, rank, world)
     if rank == 0:
         rc, full, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=3, bounces=6))
         result["equal"] = bool(np.array_equal(bits(img.numpy()), bits(full)))
+        result["equal_u8"] = bool(np.array_equal(img8.numpy(), rt.tonemap(full)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -51,6 +54,7 @@ def test_gather_rows_world2(H):
     result = mgr.dict()
     mp.spawn(_worker, args=(2, _free_port(), 24, H, result), nprocs=2, join=True)
     assert result.get("equal") is True
+    assert result.get("equal_u8") is True
 
 
 def test_weak_scaled_resolution():

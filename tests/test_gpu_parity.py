@@ -269,3 +269,25 @@ def test_offline_and_jit_lane_kernels_agree(idx):
     rc, ref, ost = oracle_render(w.scene(), cam, p)
     assert rc == 0 and np.array_equal(bits(a), bits(ref)) and np.array_equal(bits(b), bits(ref))
     assert sa.counter_dict()["visit_bvh"] == sb.counter_dict()["visit_bvh"] == ost.counter_dict()["visit_bvh"]
+
+
+def test_device_tonemap_matches_host():
+    # pixels_to_ppm bytes on the GPU == the host conversion, including specials and clamp edges
+    import torch
+    rng = np.random.default_rng(7)
+    vals = rng.uniform(-0.5, 1.6, size=(301, 7, 3)).astype(np.float32)
+    flat = vals.reshape(-1)
+    specials = np.array([0.0, -0.0, 1.0, 0.998001, 0.998002, 0.999, 1e-30, 1e-45, np.inf, -np.inf, np.nan,
+                         0.25, 0.5, 255.0 / 256.0, (255.0 / 256.0) ** 2], np.float32)
+    flat[:len(specials)] = specials
+    host = rt.tonemap(vals)
+    dev = rt.tonemap_device(torch.from_numpy(vals).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), host)
+    # a rendered frame, odd pixel count (tail path of the 4-wide kernel)
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 37, 11)
+    fb = rt.render(w.scene(), cam, rt.make_params(s, W, H, spp=4, bounces=8))
+    dev = rt.tonemap_device(torch.from_numpy(fb).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.cpu().numpy(), rt.tonemap(fb))
