@@ -143,16 +143,24 @@ __device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
   return accum;
 }
 
-template <bool LDS, bool COUNT, bool NOISE, bool UV>
+// TM: texture kinds present (bit T_*); the dispatch keeps only those
+template <bool LDS, bool COUNT, bool NOISE, bool UV, uint32_t TM = 0xfu>
 __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti, float u, float v, f3 p,
                             uint32_t &perlin_count) {
+  if (TM == (1u << T_SOLID)) {   // solid colours only: no dispatch
+    const uint4 t0 = S.w4(A.off_texs + ti * kTexWords);
+    return mk(asf(t0.y), asf(t0.z), asf(t0.w));
+  }
   for (int guard = 0; guard < 64; ++guard) {
     const uint32_t b = A.off_texs + ti * kTexWords;
     uint4 t0 = S.w4(b);
+    if (!(TM & (1u << T_CHECKER)) && !(TM & (1u << T_IMAGE)) && !(TM & (1u << T_NOISE)))
+      return mk(asf(t0.y), asf(t0.z), asf(t0.w));
     switch (t0.x) {
       case T_SOLID:
         return mk(asf(t0.y), asf(t0.z), asf(t0.w));
       case T_CHECKER: {
+        if (!(TM & (1u << T_CHECKER))) return mk(0, 0, 0);
         float inv = asf(t0.w);
         int32_t x = static_cast<int32_t>(floorf(inv * p.x));
         int32_t y = static_cast<int32_t>(floorf(inv * p.y));
@@ -161,6 +169,7 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
         ti = even ? t0.y : t0.z;
       } break;
       case T_IMAGE: {
+        if (!(TM & (1u << T_IMAGE))) return mk(0, 0, 0);
         if (!UV) return mk(1, 0, 1);        // no pixels anywhere in the scene (host-checked)
         uint4 t1 = S.w4(b + 4);
         if (t1.x == 0) return mk(1, 0, 1);
@@ -176,7 +185,7 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
         return mk(S.f(o), S.f(o + 1), S.f(o + 2));
       }
       case T_NOISE: {
-        if (!NOISE) return mk(0, 0, 0);     // unreachable: the host selects a NOISE variant
+        if (!NOISE || !(TM & (1u << T_NOISE))) return mk(0, 0, 0);   // host selects a NOISE variant
         if (COUNT) perlin_count++;
         const uint32_t tb = A.off_perlin + t0.y * kPerlinWords;
         float accum = 0.0f, weight = 1.0f;
@@ -590,6 +599,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   constexpr bool LDS = (F & kVarLds) != 0, COUNT = (F & kVarCount) != 0;
   constexpr bool NOISE = (F & kVarNoise) != 0, UV = (F & kVarUv) != 0;
   constexpr bool TRACE = (F & kVarTrace) != 0;   // per-wave timeline into A.wave_trace (diagnostics)
+  constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
+  constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
   Mem<LDS> S{A.scene};
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
@@ -787,24 +798,25 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
       const uint32_t mkind = m0.x;
       f3 emit = mk(0, 0, 0);
-      if (mkind == MAT_DIFFUSE_LIGHT) emit = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
+      if ((MM & (1u << MAT_DIFFUSE_LIGHT)) && mkind == MAT_DIFFUSE_LIGHT)
+        emit = texture_color<LDS, COUNT, NOISE, UV, TM>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
       ruv = scale(1.0f / length(ruv), ruv);
       bool scattered = false;
       f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
       const bool hfront = hit_front(h);
       const f3 hn = hfront ? h.n : flip(h.n);
-      if (mkind == MAT_LAMBERTIAN) {                                        // :458-465
+      if ((MM & (1u << MAT_LAMBERTIAN)) && mkind == MAT_LAMBERTIAN) {      // :458-465
         scattered = true;
         dir = add(hn, ruv);
         const float eps = 1e-8f;
         if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = hn;
-        att = texture_color<LDS, COUNT, NOISE, UV>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
-      } else if (mkind == MAT_METAL) {                                      // :466-472
+        att = texture_color<LDS, COUNT, NOISE, UV, TM>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
+      } else if ((MM & (1u << MAT_METAL)) && mkind == MAT_METAL) {         // :466-472
         f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, hn), hn));
         dir = add(unit(rd), scale(asf(m1.y), ruv));
         att = mk(asf(m0.z), asf(m0.w), asf(m1.x));
         scattered = dot(dir, hn) > 0;
-      } else if (mkind == MAT_DIELECTRIC) {                                 // :473-487
+      } else if ((MM & (1u << MAT_DIELECTRIC)) && mkind == MAT_DIELECTRIC) {   // :473-487
         att = mk(1.0f, 1.0f, 1.0f);
         const float ior = asf(m1.z);
         const float ri = hfront ? (1.0f / ior) : ior;

@@ -65,6 +65,9 @@ constexpr int kChunk = 64;         // pixel ids handed to a wave per work-queue 
 // register allocation (the Perlin + double-sine path alone costs ~40 VGPRs).
 enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket = 16,
              kVarTrace = 32 /* wave timeline diagnostics; scene-specialised kernels only */ };
+// run-time compiled kernels also carry the material kinds (bits 6..9, bit MAT_*) and texture kinds
+// (bits 10..13, bit T_*) present in the scene; 0 in a field means "all" (the offline kernels)
+constexpr int kVarMatShift = 6, kVarTexShift = 10;
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter

@@ -154,6 +154,7 @@ struct rt_context {
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
+  bool shade_spec = true;                       // RT_JIT_SHADE=0: run-time kernels keep every material
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
   bool fold_enabled = true;
@@ -228,6 +229,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   }
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
   if (const char *e = std::getenv("RT_JIT_LANE")) c->lane_jit = e[0] != '0';
+  if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
@@ -286,7 +288,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
-  const int trace_bit = c->wave_trace_path.empty() ? 0 : rt::kVarTrace;   // scene-specialised kernels only
+  // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
+  const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0);
   // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
   // at most jit_budget node visits (every catalog scene but the large random ones), else the per-lane
   // DFS.  The wave-packet DFS is kept as an explicit option (fastest on tiny all-sphere scenes).
@@ -557,7 +560,7 @@ int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint
   if (rc != RT_OK) return rc;
   std::string src;
   uint32_t v = 0;
-  const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0);
+  const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img);
   const bool ok = rt::jit_source(img, variant, max_visits, true, &src, &v);
   if (visits) *visits = v;
   if (!ok) return RT_ERR_UNSUPPORTED;
@@ -572,7 +575,7 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
   if (rc != RT_OK) return rc;
   std::string src, lg;
   uint32_t v = 0;
-  const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0);
+  const int variant = (img.has_noise ? rt::kVarNoise : 0) | (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img);
   if (!rt::jit_source(img, variant, max_visits, true, &src, &v)) return RT_ERR_UNSUPPORTED;
   std::vector<char> code;
   const bool ok = rt::jit_compile(src, arch, &code, &lg);

@@ -63,7 +63,7 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
                 bool *folded) {
   std::string trace;
   if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
-  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace);
+  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | (15 << kVarMatShift) | (15 << kVarTexShift));
   // RT_JIT_WAVES=N asks the register allocator for N waves per SIMD (A/B; default: unconstrained)
   std::string attr;
   if (const char *e = std::getenv("RT_JIT_WAVES"))
@@ -176,6 +176,21 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
   return build_module(src, "rt_static", out, why);
 }
 
+int scene_shading_bits(const SceneImage &img) {
+  uint32_t mm = 0, tm = 0;
+  for (uint32_t m = 0; m < img.mat_count; ++m) {
+    const uint32_t k = img.words[img.off_mats + static_cast<size_t>(m) * kMatWords + M_KIND];
+    if (k < 4) mm |= 1u << k;
+  }
+  for (uint32_t t = 0; t < img.tex_count; ++t) {
+    const uint32_t k = img.words[img.off_texs + static_cast<size_t>(t) * kTexWords + T_KIND];
+    if (k < 4) tm |= 1u << k;
+  }
+  if (mm == 0) mm = 15;   // an empty table would read as "all"; keep it explicit
+  if (tm == 0) tm = 1u << T_SOLID;
+  return static_cast<int>((mm << kVarMatShift) | (tm << kVarTexShift));
+}
+
 uint32_t scene_kinds(const SceneImage &img) {
   uint32_t km = 0;
   for (uint32_t i = 0; i < img.node_count; ++i) {
@@ -186,7 +201,7 @@ uint32_t scene_kinds(const SceneImage &img) {
 }
 
 std::string jit_lane_source(const SceneImage &img, int variant) {
-  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace);
+  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | (15 << kVarMatShift) | (15 << kVarTexShift));
   const std::string lt = "LaneTraceK<" + std::to_string(scene_kinds(img)) + "u>";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render(RenderArgs A) {\n  render_body<" +

@@ -34,6 +34,8 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
 bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
 std::string jit_lane_source(const SceneImage &img, int variant);
 uint32_t scene_kinds(const SceneImage &img);
+// material / texture kinds present, as variant bits (kVarMatShift / kVarTexShift)
+int scene_shading_bits(const SceneImage &img);
 
 // extra hipRTC options from the RT_JIT_OPTS environment variable (space separated)
 std::vector<std::string> jit_extra_options();
