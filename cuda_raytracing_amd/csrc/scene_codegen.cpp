@@ -111,10 +111,11 @@ struct Gen {
     line("{   // node " + u(i) + (tri ? " (triangle, folded)" : " (quad, folded)"));
     indent += 2;
     line("const float den" + k + " = " + val(den) + ";");
-    line("if (fabsf(den" + k + ") >= kDenomEps) {");
-    indent += 2;
-    line("const float t" + k + " = (" + f(w[W_D]) + " - " + val(non) + ") / den" + k + ";");
-    line("if (kTmin <= t" + k + " && t" + k + " <= T.tmax) {");
+    // t for every lane (a tiny denominator only yields inf/NaN there), one branch for both tests
+    // dd - x with dd = +-0 is -x up to the sign of a zero t (which fails the tmin test either way)
+    const std::string num = is_zero(w[W_D]) ? "(-" + val(non) + ")" : "(" + f(w[W_D]) + " - " + val(non) + ")";
+    line("const float t" + k + " = " + num + " / den" + k + ";");
+    line("if ((fabsf(den" + k + ") >= kDenomEps) & (kTmin <= t" + k + ") & (t" + k + " <= T.tmax)) {");
     indent += 2;
     line("const f3 p" + k + " = mk(r.o.x + r.d.x * t" + k + ", r.o.y + r.d.y * t" + k + ", r.o.z + r.d.z * t" + k + ");");
     const char *ax[3] = {"x", "y", "z"};
@@ -153,8 +154,6 @@ struct Gen {
     line("h.u = al" + k + "; h.v = be" + k + "; h.t = t" + k + "; h.p = p" + k + "; h.mat = " + u(w[W_AUX]) + ";");
     line("h.fd = den" + k + "; h.n = " + v3(w, W_NORMAL) + ";   // dot(dir, n) == denom bitwise (same products)");
     line(std::string("T.tmax = t") + k + ";" + (in_xf ? " T.was_last = 1;" : ""));
-    indent -= 2;
-    line("}");
     indent -= 2;
     line("}");
     indent -= 2;
