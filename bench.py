@@ -143,6 +143,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle wall time (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=2, help="frames queued at once (own context + stream each)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (plumbing rehearsal)")
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,9 +151,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
+    dev = local_rank % max(torch.cuda.device_count(), 1)   # == local_rank on a node with a GPU per rank
+    torch.cuda.set_device(dev)
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":   # RCCL over xGMI, one rank per GPU
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:                             # rehearsal of the multi-rank plumbing (CPU collectives)
+            dist.init_process_group(args.dist_backend)
 
     # ---- host pre-pass (untimed, like the reference's make_bvh + camera) ----
     world, settings = rt.build_scene(args.scene)
@@ -162,7 +167,7 @@ def main():
     params = rt.make_params(settings, W, H, spp=args.spp, bounces=args.bounces,
                             row_offset=off, row_stride=stride, row_count=rows)
     nf = max(1, args.inflight)
-    ctxs = [rt.RenderContext(world.scene(), device=local_rank) for _ in range(nf)]
+    ctxs = [rt.RenderContext(world.scene(), device=dev) for _ in range(nf)]
     ctx = ctxs[0]
     streams = [torch.cuda.Stream() for _ in range(nf)]
     outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nf)]
@@ -197,7 +202,10 @@ def main():
         st = ctxs[i].timing()                                  # waits on that frame's render events
         torch.cuda.current_stream().wait_stream(streams[i])    # ... and its tonemap
         if world_size > 1:
-            gather_rows(outs8[i], H, W, rank, world_size)      # u8 rows: 3 B/pixel over xGMI
+            if args.dist_backend == "nccl":
+                gather_rows(outs8[i], H, W, rank, world_size)  # u8 rows: 3 B/pixel over xGMI
+            else:
+                gather_rows(outs8[i].cpu(), H, W, rank, world_size)
         stats.append(st)
 
     def run(frames):
@@ -225,6 +233,8 @@ def main():
     elapsed = time.perf_counter() - t0
     if world_size > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        if args.dist_backend != "nccl":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     render_ms = [st.render_ms for st in stats]
@@ -254,7 +264,7 @@ def main():
             "config": {
                 "workload": workload,
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
-                "parallelism": f"rows interleaved x{world_size}" + (" + RCCL u8 gather" if world_size > 1 else ""),
+                "parallelism": f"rows interleaved x{world_size}" + ((" + RCCL u8 gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} u8 gather") if world_size > 1 else ""),
                 "output": "PPM bytes on the device (rt_tonemap_device)",
                 "pixels_per_gpu": rows * W,
                 "frames_in_flight": nf,
