@@ -32,7 +32,7 @@ ctxs = {}
 for c in a.configs.split(","):
     saved = dict(os.environ)
     for kv in c.split(";"):
-        k, v = kv.split("=")
+        k, v = kv.split("=", 1)
         os.environ[k] = v
     ctxs[c] = rt.RenderContext(w.scene(), 0)
     os.environ.clear(); os.environ.update(saved)
