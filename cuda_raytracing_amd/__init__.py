@@ -86,6 +86,12 @@ class World:
     def image(self, name: str = "earthmap.jpg") -> _abi.Material:
         return self._L.rt_mat_lambert_image(self._w, name.encode())
 
+    def image_pixels(self, rgb) -> _abi.Material:
+        """Image texture with texels (float32 [H, W, 3], like stbi_loadf) — copied into the arena."""
+        a = np.ascontiguousarray(rgb, dtype=np.float32)
+        self._keep = getattr(self, "_keep", []) + [a]
+        return self._L.rt_mat_lambert_image_pixels(self._w, a.ctypes.data_as(C.c_void_p), a.shape[1], a.shape[0])
+
     def metal(self, rgb, fuzz: float) -> _abi.Material:
         return self._L.rt_mat_metal(vec3(*rgb), fuzz)
 

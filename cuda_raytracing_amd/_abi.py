@@ -140,6 +140,7 @@ def host_lib():
         for name in ("rt_mat_lambert_solid", "rt_mat_light_solid"):
             _sig(getattr(L, name), Material, P, Vec3)
         _sig(L.rt_mat_lambert_image, Material, P, C.c_char_p)
+        _sig(L.rt_mat_lambert_image_pixels, Material, P, P, C.c_int32, C.c_int32)
         _sig(L.rt_mat_lambert_noise, Material, P, C.c_float)
         _sig(L.rt_mat_metal, Material, Vec3, C.c_float)
         _sig(L.rt_mat_dielectric, Material, C.c_float)
@@ -219,6 +220,8 @@ def oracle_lib():
              C.c_void_p, C.POINTER(Stats))
         _sig(L.rt_oracle_sinf, C.c_float, C.c_float)
         _sig(L.rt_oracle_pow5f, C.c_float, C.c_float)
+        _sig(L.rt_oracle_atan2f, C.c_float, C.c_float, C.c_float)
+        _sig(L.rt_oracle_acosf, C.c_float, C.c_float)
         _sig(L.rt_oracle_uniforms, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int)
         _sig(L.rt_oracle_threads, C.c_int)
         _oracle = L

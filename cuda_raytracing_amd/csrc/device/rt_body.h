@@ -109,6 +109,66 @@ __device__ __forceinline__ float rt_pow5f(float xf) {   // powf(x, 5.0f) substit
   return static_cast<float>(x4 * x);
 }
 
+// acosf / atan2f substitutes (sphere_get_uv, :583-590; only image textures read u,v): the float
+// rounding of a double evaluation built from + - * and float seeds only, so the oracle and the HIP
+// kernel (device/rt_body.h, the same operations) produce identical bits.  atan on [0,1]: anchor
+// c = k/8, r = (t - c)/(1 + t c) (|r| <= 1/16), odd Taylor series to r^15 (error < 3e-22).
+__device__ constexpr double RT_ATAN_K8[9] = {0.0, 0.12435499454676144, 0.24497866312686414, 0.35877067027057225,
+                                     0.4636476090008061, 0.5585993153435624, 0.6435011087932844,
+                                     0.7188299996216245, 0.7853981633974483};
+__device__ __forceinline__ double rt_recip_d(double x) {            /* 1/x, x in [2^-60, 2^60]: float seed + 2 Newton steps */
+  double y = (double)(1.0f / (float)x);
+  y = y * (2.0 - x * y);
+  y = y * (2.0 - x * y);
+  return y;
+}
+__device__ __forceinline__ double rt_atan01_d(double t) {           /* t in [0, 1] */
+  int k = (int)(t * 8.0 + 0.5);
+  double c = (double)k * 0.125;
+  double r = (t - c) * rt_recip_d(1.0 + t * c);
+  double r2 = r * r;
+  double p = r * (1.0 + r2 * (-1.0 / 3.0 + r2 * (1.0 / 5.0 + r2 * (-1.0 / 7.0 + r2 * (1.0 / 9.0 +
+             r2 * (-1.0 / 11.0 + r2 * (1.0 / 13.0 + r2 * (-1.0 / 15.0))))))));
+  return RT_ATAN_K8[k] + p;
+}
+__device__ __forceinline__ double rt_atan2_d(double y, double x) {  /* finite, not both zero */
+  const double pi = 3.141592653589793, half_pi = 1.5707963267948966;
+  double ax = fabs(x), ay = fabs(y);
+  double m = ax > ay ? ax : ay;
+  if (m < 8.673617379884035e-19) { ax *= 1.2676506002282294e30; ay *= 1.2676506002282294e30; }   /* 2^-60, 2^100 */
+  else if (m > 1.152921504606847e18) { ax *= 7.888609052210118e-31; ay *= 7.888609052210118e-31; } /* 2^60, 2^-100 */
+  double a;
+  if (ay <= ax) a = rt_atan01_d(ay * rt_recip_d(ax));
+  else a = half_pi - rt_atan01_d(ax * rt_recip_d(ay));
+  if (x < 0.0 || (x == 0.0 && __builtin_signbit(x))) a = pi - a;
+  return __builtin_signbit(y) ? -a : a;
+}
+__device__ __forceinline__ float rt_atan2f(float yf, float xf) {
+  const double pi = 3.141592653589793;
+  if (__builtin_isnan(xf) || __builtin_isnan(yf)) return xf + yf;
+  double x = (double)xf, y = (double)yf, r;
+  if (x == 0.0 && y == 0.0) r = __builtin_signbit(x) ? pi : 0.0;
+  else if (__builtin_isinf(xf) && __builtin_isinf(yf)) r = x > 0.0 ? 0.7853981633974483 : 2.356194490192345;
+  else if (__builtin_isinf(xf)) r = x > 0.0 ? 0.0 : pi;
+  else if (__builtin_isinf(yf)) r = 1.5707963267948966;
+  else return (float)rt_atan2_d(y, x);
+  return (float)(__builtin_signbit(y) ? -r : r);
+}
+__device__ __forceinline__ float rt_acosf(float xf) {
+  if (!(fabsf(xf) <= 1.0f)) return (xf - xf) / (xf - xf);   /* NaN */
+  double x = (double)xf;
+  double s = (1.0 - x) * (1.0 + x);
+  double q = 0.0;
+  if (s > 0.0) {
+    double r = (double)(1.0f / sqrtf((float)s));
+    r = r * (1.5 - 0.5 * s * r * r);
+    r = r * (1.5 - 0.5 * s * r * r);
+    q = s * r;
+  }
+  if (q == 0.0) return xf > 0.0f ? 0.0f : 3.14159274101257324f;   /* acos(1) = 0, acos(-1) = pi */
+  return (float)rt_atan2_d(q, x);
+}
+
 // ---------------------------------------------------------------------------------------------
 // textures + Perlin (raytracing.cu:343-398, perlin_noise.cpp:1-46,72-85)
 // ---------------------------------------------------------------------------------------------
@@ -314,8 +374,8 @@ __device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32
       f3 outward = scale(inv_rad, sub(h.p, center));
       if (UV) {
         const float pi = 3.1415926535897932385f;
-        float theta = acosf(-outward.y);
-        float phi = atan2f(-outward.z, outward.x) + pi;
+        float theta = rt_acosf(-outward.y);
+        float phi = rt_atan2f(-outward.z, outward.x) + pi;
         h.u = phi / (2 * pi);
         h.v = theta / pi;
       }
@@ -348,8 +408,8 @@ __device__ __forceinline__ void sphere_hit_static(Trav &T, const Ray &r, Hit &h,
       f3 outward = scale(inv_rad, sub(h.p, center));
       if (UV) {
         const float pi = 3.1415926535897932385f;
-        float theta = acosf(-outward.y);
-        float phi = atan2f(-outward.z, outward.x) + pi;
+        float theta = rt_acosf(-outward.y);
+        float phi = rt_atan2f(-outward.z, outward.x) + pi;
         h.u = phi / (2 * pi);
         h.v = theta / pi;
       }

@@ -446,6 +446,18 @@ rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name) {
   t.kind = RTR_TEX_IMAGE;
   return mat_with_tex(RTR_MAT_LAMBERTIAN, w->texture_add(t, nullptr, nullptr, 0));
 }
+rtr_material rt_mat_lambert_image_pixels(rt_world *w, const float *rgb, int32_t width, int32_t height) {
+  // what make_image_texture (:332-341) builds when stbi_loadf succeeds: float RGB texels copied into
+  // the arena behind the Texture record (texture_list_add, :270-279)
+  rtr_texture t; std::memset(&t, 0, sizeof t);
+  t.kind = RTR_TEX_IMAGE;
+  if (!rgb || width <= 0 || height <= 0) return mat_with_tex(RTR_MAT_LAMBERTIAN, w->texture_add(t, nullptr, nullptr, 0));
+  t.u.image.host_pixels = reinterpret_cast<uint64_t>(rgb);
+  t.u.image.width = width;
+  t.u.image.height = height;
+  return mat_with_tex(RTR_MAT_LAMBERTIAN,
+                      w->texture_add(t, nullptr, rgb, static_cast<uint64_t>(width) * static_cast<uint64_t>(height)));
+}
 rtr_material rt_mat_lambert_noise(rt_world *w, float scale) {
   rtr_perlin p;
   w->make_perlin(&p);

@@ -62,6 +62,8 @@ int32_t rt_world_rand(rt_world *w);
 rtr_material rt_mat_lambert_solid(rt_world *w, rtr_vec3 albedo);                 /* :1805 */
 rtr_material rt_mat_light_solid(rt_world *w, rtr_vec3 color);                    /* :1813 */
 rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name);           /* :1821 */
+/* an image texture whose load succeeded: width*height float RGB texels (stbi_loadf layout, row 0 first) */
+rtr_material rt_mat_lambert_image_pixels(rt_world *w, const float *rgb, int32_t width, int32_t height);
 rtr_material rt_mat_lambert_noise(rt_world *w, float scale);                     /* :1829 */
 rtr_material rt_mat_metal(rtr_vec3 albedo, float fuzz);                          /* :516 */
 rtr_material rt_mat_dielectric(float ior);                                       /* :524 */

@@ -79,3 +79,18 @@ def params_for(case, manifest):
 
 def bits(a):
     return np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
+
+
+def image_scene():
+    """Spheres and quads with a synthetic image texture (the reference's earthmap.jpg is absent):
+    exercises sphere_get_uv (rt_acosf / rt_atan2f), planar u,v and image_texture_get_pixel's clamp."""
+    import cuda_raytracing_amd as rt
+    w = rt.World(capacity=64)
+    yy, xx = np.mgrid[0:19, 0:37].astype(np.float32)
+    tex = np.stack([xx / 36.0, yy / 18.0, 0.25 + 0.5 * ((xx + yy) % 3 == 0)], axis=-1).astype(np.float32)
+    img = w.image_pixels(tex)
+    w.sphere((0, 0, -2), 0.8, img)
+    w.sphere((1.2, 0.3, -2.5), 0.5, img)
+    w.quad((-3, -1, -4), (6, 0, 0), (0, 0, 3.5), img)
+    w.sphere((-1.3, 0.2, -1.8), 0.4, w.metal((0.8, 0.8, 0.8), 0.1))
+    return w

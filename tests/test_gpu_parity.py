@@ -291,3 +291,21 @@ def test_device_tonemap_matches_host():
     dev = rt.tonemap_device(torch.from_numpy(fb).cuda())
     torch.cuda.synchronize()
     assert np.array_equal(dev.cpu().numpy(), rt.tonemap(fb))
+
+
+def test_image_texture_scene_vs_oracle():
+    # image textures with texels (UV variant: rt_acosf / rt_atan2f, planar u,v, texel clamp) — every
+    # traversal policy against the oracle
+    from conftest import image_scene
+    w = image_scene()
+    s = rt.Settings()
+    _abi.host_lib().rt_settings_default(C.byref(s))
+    s.lookfrom, s.lookat, s.vfov = rt.vec3(0, 0, 0), rt.vec3(0, 0, -1), 90.0
+    cam, W, H = rt.camera_from_settings(s, 40, 24)
+    p = rt.make_params(s, W, H, spp=4, bounces=6)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and len(np.unique(ref.reshape(-1, 3), axis=0)) > 50
+    for force, _want in TRAVERSALS:
+        p.flags = force
+        fb, _ = gpu(w.scene(), cam, p)
+        assert np.array_equal(bits(fb), bits(ref)), force

@@ -158,3 +158,32 @@ def test_oracle_stack_within_reference_allocation():
         _, _, st = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=2, bounces=8))
         assert st.counter_dict()["max_stack"] <= w.reference_stack_depth()
         assert st.counter_dict()["max_stack"] <= want
+
+
+def test_atan2_acos_substitutes_are_correctly_rounded():
+    # rt_atan2f / rt_acosf (sphere_get_uv, image textures only): correctly rounded on every sample,
+    # and the exact IEEE special cases of atan2f/acosf
+    import math
+    L = _abi.oracle_lib()
+    rng = np.random.default_rng(11)
+    ys = np.concatenate([rng.uniform(-1, 1, 20000), rng.uniform(-1e3, 1e3, 5000)]).astype(np.float32)
+    xs = np.concatenate([rng.uniform(-1, 1, 20000), rng.uniform(-1e-3, 1e-3, 5000)]).astype(np.float32)
+    for y, x in zip(ys, xs):
+        assert np.float32(L.rt_oracle_atan2f(float(y), float(x))) == np.float32(math.atan2(float(y), float(x)))
+    for x in np.concatenate([rng.uniform(-1, 1, 20000), 1 - rng.uniform(0, 1e-4, 2000)]).astype(np.float32):
+        assert np.float32(L.rt_oracle_acosf(float(x))) == np.float32(math.acos(float(x)))
+    for y, x in [(0.0, 0.0), (-0.0, 0.0), (0.0, -0.0), (-0.0, -0.0), (1.0, -0.0), (1e-40, 1e-40), (3e38, 1.0),
+                 (math.inf, math.inf), (-math.inf, 1.0), (1.0, -math.inf)]:
+        got, want = np.float32(L.rt_oracle_atan2f(y, x)), np.float32(math.atan2(y, x))
+        assert got == want and np.signbit(got) == np.signbit(want), (y, x)
+    assert L.rt_oracle_acosf(1.0) == 0.0 and np.float32(L.rt_oracle_acosf(-1.0)) == np.float32(math.pi)
+    assert math.isnan(L.rt_oracle_acosf(1.5))
+
+
+def test_image_texture_scene_renders():
+    from conftest import image_scene
+    w = image_scene()
+    fb, _ = _render(w, W=24, H=16, spp=4, b=6)
+    assert np.isfinite(fb).all() and fb.max() > 0
+    # not the magenta of a missing image: the texel gradient shows up
+    assert len(np.unique(fb.reshape(-1, 3), axis=0)) > 50
