@@ -697,7 +697,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool exhausted = false;
   uint32_t tiles_taken = 0, rounds = 0;
   uint32_t probe_tile = 0, probe_rounds = 0;
-  uint64_t ph_refill = 0, ph_trace = 0, ph_mat = 0, ph_shade = 0, t_mark = 0;   // wave-trace phase clocks
+  uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, t_mark = 0;   // wave-trace clocks
   uint64_t busy_lane_rounds = 0;
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
 
@@ -853,6 +853,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       pending = got ? 0u : 1u;
     }
+    if (TRACE) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      ph_rej += t - t_mark;
+      t_mark = t;
+    }
     if (T.result && !pending) {
       const uint32_t mbase = A.off_mats + h.mat * kMatWords;
       const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
@@ -976,7 +981,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     unsigned long long *w = A.wave_trace + kWaveTraceWords * static_cast<size_t>(blockIdx.x * kWavesPerBlock + wave);
     w[0] = t_start; w[1] = t_end; w[2] = tiles_taken; w[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
     w[4] = rounds; w[5] = busy_lane_rounds;
-    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade; w[9] = ph_mat;
+    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade; w[9] = ph_mat; w[10] = ph_rej;
   }
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};

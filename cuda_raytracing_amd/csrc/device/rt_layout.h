@@ -70,8 +70,8 @@ enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket =
 constexpr int kVarMatShift = 6, kVarTexShift = 10;
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
-// refill / traversal / unwind+accumulate+next camera ray / material scatter
-constexpr uint32_t kWaveTraceWords = 10;
+// refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
+constexpr uint32_t kWaveTraceWords = 11;
 
 // Resident 256-thread blocks per CU allowed by the VGPR budget: 512 VGPRs per lane per SIMD, one
 // wave of each block per SIMD.  The persistent grid must never exceed residency (a block that starts

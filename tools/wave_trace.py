@@ -27,7 +27,7 @@ import cuda_raytracing_amd as rt  # noqa: E402
 w, s = rt.build_scene(a.scene)
 cam, W, H = rt.camera_from_settings(s, a.width, a.height)
 fb, st = rt.render(w.scene(), cam, rt.make_params(s, W, H, spp=a.spp, bounces=a.bounces), with_stats=True)
-rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 10)
+rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 11)
 rec = rec[rec[:, 1] > 0]
 t0 = rec[:, 0].min()
 start = (rec[:, 0] - t0).astype(np.float64)
@@ -42,8 +42,8 @@ tiles = rec[:, 2].astype(np.int64)
 print("tiles/wave: min %d mean %.2f max %d" % (tiles.min(), tiles.mean(), tiles.max()))
 rounds = rec[:, 4].astype(np.float64); busy = rec[:, 5].astype(np.float64)
 print("busy lanes per round (wave mean): %.1f of 64; rounds/wave mean %.0f" % (busy.sum() / rounds.sum(), rounds.mean()))
-ph = rec[:, 6:10].astype(np.float64).sum(axis=0)
-print("phase cycles: refill %.1f%%  traverse %.1f%%  unwind+camera %.1f%%  material+scatter %.1f%%"
+ph = rec[:, 6:11].astype(np.float64).sum(axis=0)
+print("phase cycles: refill %.1f%%  traverse %.1f%%  unwind+camera %.1f%%  material+scatter %.1f%%  rejection %.1f%%"
       % tuple(100 * ph / ph.sum()))
 xcc = (rec[:, 3] >> np.uint64(32)).astype(np.int64)
 for x in np.unique(xcc):
