@@ -62,20 +62,37 @@ struct Mem {
 // ---------------------------------------------------------------------------------------------
 // RNG: rocRAND XORWOW (replaces cuRAND)
 // ---------------------------------------------------------------------------------------------
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); LLVM does not form it for
+// 32-bit xor chains by itself
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 struct Rng {
   uint32_t d, x0, x1, x2, x3, x4;
   __device__ __forceinline__ uint32_t next() {
     uint32_t t = x0 ^ (x0 >> 2);
     x0 = x1; x1 = x2; x2 = x3; x3 = x4;
-    x4 = (x4 ^ (x4 << 4)) ^ (t ^ (t << 1));
+    x4 = xor3(x4, x4 << 4, t) ^ (t << 1);
     d += 362437u;
     return d + x4;
   }
-  __device__ __forceinline__ float uniform() {       // rocrand_uniform: (0, 1]
+  // rocrand_uniform: inv + f*inv with f = (float)v, inv = 2^-32 — in (0, 1].  f*inv is exact (a
+  // power-of-two scale of a float >= 1), so one fma with the same operands rounds identically to the
+  // reference's multiply-then-add: this is an exact rewrite, not a contraction.
+  __device__ __forceinline__ float uniform() {
     const float inv = 2.3283064e-10f;
-    return inv + (static_cast<float>(next()) * inv);
+    return __builtin_fmaf(static_cast<float>(next()), inv, inv);
   }
   __device__ __forceinline__ float bound(float lo, float hi) { return lo + (hi - lo) * uniform(); }
+  // bound(-1, 1) = -1 + 2*uniform(); 2*uniform() = fl(2inv + f*2inv) exactly (scaling by 2 commutes
+  // with rounding), again a single exact fma
+  __device__ __forceinline__ float sym() {
+    const float inv2 = 4.6566129e-10f;   // 2^-31
+    return -1.0f + __builtin_fmaf(static_cast<float>(next()), inv2, inv2);
+  }
 };
 
 // sinf substitute (identical algorithm in the oracle: float rounding of a double sine)
@@ -718,8 +735,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     } else {                                                                // :1459-1476
       float x, y;
       for (;;) {
-        y = rng.bound(-1.0f, 1.0f);    // Vec3(x(), y(), 0): y drawn first
-        x = rng.bound(-1.0f, 1.0f);
+        y = rng.sym();    // bound(-1, 1); Vec3(x(), y(), 0): y drawn first
+        x = rng.sym();
         float l = sqrtf(x * x + y * y + 0.0f * 0.0f);
         if (l * l < 1.0f) break;
       }
@@ -834,9 +851,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       bool got = false;
       for (uint32_t k = 0; k != try_cap; ++k) {
-        float z = rng.bound(-1.0f, 1.0f);
-        float y = rng.bound(-1.0f, 1.0f);
-        float x = rng.bound(-1.0f, 1.0f);
+        float z = rng.sym();   // bound(-1, 1)
+        float y = rng.sym();
+        float x = rng.sym();
         // accept iff fl(fl(sqrt(s))^2) in (0, 1] (vec3.h:152-161, `1e-50 < len2` == `len2 > 0`).
         // Decided on s itself except within 2^-20 of 1: s in (0, 1-2^-20] always passes, s >= 1+2^-20
         // always fails (components are 0 or >= 2^-31 in magnitude, so s > 0 => len2 > 0); the sqrt and
