@@ -13,7 +13,7 @@ step() {  # name, limit, command...
 }
 SKIP_TESTS=${SKIP_TESTS:-0}
 if [ "$SKIP_TESTS" != 1 ]; then
-  step pytest_gpu 900 python3 -m pytest tests -q -m gpu
+  step pytest_gpu 900 python3 -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench 900 python3 bench.py ${BENCH_ARGS:-}
