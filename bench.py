@@ -249,7 +249,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "Msamples/sec (pixels x spp / s) at 1920x1080 spp=512 d=16",
+            "metric": f"Msamples/sec (pixels x spp / s) at {args.width}x{args.height} spp={args.spp} d={args.bounces}"
+                      + (f" scene {args.scene}" if args.scene != 0 else ""),
             "value": round(value, 2),
             "unit": "Msamples/s",
             "n_gpus": world_size,

@@ -849,26 +849,33 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         if (COUNT) c_shade++;
         random_test = rng.uniform();
       }
-      bool got = false;
-      for (uint32_t k = 0; k != try_cap; ++k) {
-        float z = rng.sym();   // bound(-1, 1)
-        float y = rng.sym();
-        float x = rng.sym();
-        // accept iff fl(fl(sqrt(s))^2) in (0, 1] (vec3.h:152-161, `1e-50 < len2` == `len2 > 0`).
-        // Decided on s itself except within 2^-20 of 1: s in (0, 1-2^-20] always passes, s >= 1+2^-20
-        // always fails (components are 0 or >= 2^-31 in magnitude, so s > 0 => len2 > 0); the sqrt and
-        // the division run once, after the loop, instead of on every try of every lane.
-        const float s2 = x * x + y * y + z * z;
-        bool acc = s2 > 0.0f && s2 <= 0.99999904632568359375f;           // 1 - 2^-20
-        const bool near1 = s2 > 0.99999904632568359375f && s2 < 1.00000095367431640625f;
-        if (__ballot(near1) != 0) {   // wave-uniform branch: keeps the rare exact test out of the loop
-          asm volatile("" ::: "memory");   // not speculated (the compiler would if-convert the sqrt)
-          const float l = sqrtf(s2);
-          if (near1) acc = l * l <= 1.0f;
+      // Wave-uniform loop: one try per iteration for every lane still rejecting.  It ends when no
+      // lane needs a try, after try_cap tries, or once at most A.defer_lanes lanes are left (those
+      // resume next round): the wave no longer runs the maximum of 64 geometric try counts.
+      bool want = true;
+      for (uint32_t k = 0;;) {
+        if (want) {
+          float z = rng.sym();   // bound(-1, 1)
+          float y = rng.sym();
+          float x = rng.sym();
+          // accept iff fl(fl(sqrt(s))^2) in (0, 1] (vec3.h:152-161, `1e-50 < len2` == `len2 > 0`).
+          // Decided on s itself except within 2^-20 of 1: s in (0, 1-2^-20] always passes, s >= 1+2^-20
+          // always fails (components are 0 or >= 2^-31 in magnitude, so s > 0 => len2 > 0); the sqrt and
+          // the division run once, after the loop, instead of on every try of every lane.
+          const float s2 = x * x + y * y + z * z;
+          bool acc = s2 > 0.0f && s2 <= 0.99999904632568359375f;           // 1 - 2^-20
+          const bool near1 = s2 > 0.99999904632568359375f && s2 < 1.00000095367431640625f;
+          if (__ballot(near1) != 0) {   // wave-uniform branch: keeps the rare exact test out of the loop
+            asm volatile("" ::: "memory");   // not speculated (the compiler would if-convert the sqrt)
+            const float l = sqrtf(s2);
+            if (near1) acc = l * l <= 1.0f;
+          }
+          if (acc) { ruv = mk(x, y, z); want = false; }
         }
-        if (acc) { ruv = mk(x, y, z); got = true; break; }
+        const uint64_t left = __ballot(want);
+        if (left == 0 || ++k == try_cap || static_cast<uint32_t>(__popcll(left)) <= A.defer_lanes) break;
       }
-      pending = got ? 0u : 1u;
+      pending = want ? 1u : 0u;
     }
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();

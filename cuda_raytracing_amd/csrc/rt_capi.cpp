@@ -153,6 +153,7 @@ struct rt_context {
   bool rc_lds_auto = true;                      // RT_RC_LDS_LEVELS given: exactly that many
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
+  uint32_t defer_lanes = 4;                     // RT_DEFER_LANES: end a round's rejection at <= this many lanes
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
   bool shade_spec = true;                       // RT_JIT_SHADE=0: run-time kernels keep every material
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
@@ -231,6 +232,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_LANE")) c->lane_jit = e[0] != '0';
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+  if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
@@ -411,6 +413,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.fold_violation = static_cast<uint32_t *>(c->work.p) + 15;   // zeroed with the work counters
   a.black_skip = c->black_skip ? 1u : 0u;
   a.max_tries = c->max_tries;
+  a.defer_lanes = c->defer_lanes;
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;

@@ -242,11 +242,14 @@ def test_folded_and_unfolded_static_traversal(idx):
         assert sa.folded == 1 and sb.folded == 0 and sa.fold_rerenders == 0
 
 
-@pytest.mark.parametrize("tries", ["1", "2", "3"])
+@pytest.mark.parametrize("tries", ["1", "2", "3", "0/4", "0/63", "3/2"])
 @pytest.mark.parametrize("idx", [0, 1, 8])
 def test_capped_rejection_tries_agree(idx, tries, monkeypatch):
-    # deferring an unfinished rejection loop to the next round must not change any draw or result
-    monkeypatch.setenv("RT_MAX_TRIES", tries)
+    # deferring an unfinished rejection loop to the next round (after RT_MAX_TRIES tries, or once at
+    # most RT_DEFER_LANES lanes still reject) must not change any draw or result
+    cap, _, defer = tries.partition("/")
+    monkeypatch.setenv("RT_MAX_TRIES", cap)
+    monkeypatch.setenv("RT_DEFER_LANES", defer or "0")
     w, s = rt.build_scene(idx)
     cam, W, H = rt.camera_from_settings(s, 33, 19)
     for force in (rt.RT_FLAG_FORCE_STATIC, rt.RT_FLAG_FORCE_LANE):
