@@ -95,6 +95,31 @@ struct Rng {
   }
 };
 
+// ---------------------------------------------------------------------------------------------
+// correctly rounded f32 division, split so that one denominator's reciprocal can serve several
+// numerators.  The compiler's a/b (-fhip-fp32-correctly-rounded-divide-sqrt) is
+//   b' = div_scale(b), a' = div_scale(a), r0 = rcp(b'), r = fma(fma(-b', r0, 1), r0, r0),
+//   q = a'*r, q = fma(fma(-b', q, a'), r, q), q = div_fmas(fma(-b', q, a'), r, q), div_fixup(q, b, a).
+// When neither div_scale scales (b and 1/b normal, a not tiny, exponent gap < 96, quotient normal)
+// div_scale returns its operand, div_fmas is a plain fma and div_fixup returns q: rcp_ref + div_ref
+// below are then that very instruction sequence minus the identities, i.e. bit-identical to a/b.
+// Callers use them only where the operands of every lane whose result matters are in that range.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float rcp_ref(float b) {
+  const float r0 = __builtin_amdgcn_rcpf(b);
+  return __builtin_fmaf(__builtin_fmaf(-b, r0, 1.0f), r0, r0);
+}
+__device__ __forceinline__ float div_ref(float a, float b, float r) {   // r = rcp_ref(b)
+  float q = a * r;
+  q = __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+  return __builtin_fmaf(__builtin_fmaf(-b, q, a), r, q);
+}
+// |b| in [2^-60, 2^60]: 1/b by div_ref equals 1.0f/b (NaN and 0 fail the test)
+__device__ __forceinline__ bool recip_safe(float b) {
+  const float a = fabsf(b);
+  return (a >= 8.67361737988403547206e-19f) & (a <= 1.15292150460684697600e+18f);
+}
+
 // sinf substitute (identical algorithm in the oracle: float rounding of a double sine)
 __device__ __forceinline__ float rt_sinf(float xf) {
   double x = static_cast<double>(xf);
@@ -298,6 +323,7 @@ struct Visits { uint32_t k[7]; uint32_t max_sp; };
 // locals of hit() (:1082-1088) plus a cached 1/dir
 struct Trav {
   f3 inv;          // 1/dir, refreshed whenever the ray direction changes (y-rotation enter/exit)
+  f3 rcp;          // rcp_ref(dir) (scene-specialised folded traversal: shared by axis-aligned planes)
   float tmax;      // shrinking ray_tmax (closest hit so far)
   int sp;          // per-lane hit-stack depth (0 = traversal finished)
   int tc, yc;      // translation / y-rotation cleanup counters
@@ -311,6 +337,18 @@ __device__ __forceinline__ void trav_reset(Trav &T, const Ray &r) {
   T.sp = 0;
   T.tc = 0; T.yc = 0;
   T.was_last = 0; T.result = false;
+}
+
+// 1/dir through the shared reciprocals (folded scene-specialised traversal); a lane with a tiny,
+// zero or huge component takes the exact division (wave-uniform branch, normally never taken)
+__device__ __forceinline__ void dir_rcp(Trav &T, const Ray &r) {
+  T.rcp = mk(rcp_ref(r.d.x), rcp_ref(r.d.y), rcp_ref(r.d.z));
+  T.inv = mk(div_ref(1.0f, r.d.x, T.rcp.x), div_ref(1.0f, r.d.y, T.rcp.y), div_ref(1.0f, r.d.z, T.rcp.z));
+  const bool bad = !(recip_safe(r.d.x) && recip_safe(r.d.y) && recip_safe(r.d.z));
+  if (__ballot(bad) != 0) {
+    asm volatile("" ::: "memory");   // keep the exact divisions off the common path
+    if (bad) T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+  }
 }
 
 // the same without 1/dir (scene-specialised traversal: computed lazily before box tests)
@@ -591,10 +629,10 @@ __device__ __forceinline__ void wpush(WStack &W, uint32_t lane, uint32_t node, u
 
 struct PacketTrace {
   template <bool LDS, bool COUNT, bool UV>
-  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &A, bool, uint64_t lanes,
+  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &A, bool busy, uint64_t lanes,
                                              uint32_t lane, uint16_t *, Trav &T, Ray &r, Hit &h, Visits &vc) {
     cnode_ptr nodes = (cnode_ptr)(reinterpret_cast<uintptr_t>(A.scene));
-    trav_reset(T, r);
+    if (busy) trav_reset(T, r);   // a lane resuming its rejection sampling keeps its hit
     WStack W{0, 0, 0, 0};
     wpush(W, lane, A.root, lanes);
     int depth_seen = 1;
@@ -704,7 +742,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
   f3 sum = mk(0, 0, 0);
   Trav T;
-  T.inv = mk(0, 0, 0); T.tmax = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = 0; T.result = false;
+  T.inv = mk(0, 0, 0); T.rcp = mk(0, 0, 0); T.tmax = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = 0; T.result = false;
   Hit h;
   h.u = 0; h.v = 0; h.t = 0; h.fd = 0; h.mat = 0; h.p = mk(0, 0, 0); h.n = mk(0, 0, 0);
   Visits vc{};

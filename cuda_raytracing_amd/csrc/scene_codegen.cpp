@@ -61,8 +61,12 @@ struct Gen {
   // cache it in T.inv.  Here it is (re)computed only before a box test that follows a direction change
   // (start, y-rotation enter/exit), instead of at every rotation — same values, fewer divisions.
   bool inv_fresh = false;
-  std::vector<uint32_t> boxes_after;   // boxes_after[k]: BVH visits after pre-order visit k (pass 1)
-  std::vector<uint8_t> kinds;          // pass 1: kind of pre-order visit k (1-based)
+  // A/B knobs: RT_JIT_FASTDIV=0 keeps the compiler's division in the folded copy; RT_JIT_SHARE_RCP=0
+  // gives every axis-aligned plane its own reciprocal instead of the direction's shared one
+  bool fast_div = !(std::getenv("RT_JIT_FASTDIV") && std::getenv("RT_JIT_FASTDIV")[0] == '0');
+  bool share_rcp = fast_div && !(std::getenv("RT_JIT_SHARE_RCP") && std::getenv("RT_JIT_SHARE_RCP")[0] == '0');
+  std::vector<uint32_t> boxes_after;   // boxes_after[k]: visits reading 1/dir after pre-order visit k (pass 1)
+  std::vector<uint8_t> kinds;          // pass 1: 1 if pre-order visit k (1-based) reads 1/dir
   bool collect = false;
 
   bool span1_primitive(const uint32_t *w) const {
@@ -72,8 +76,27 @@ struct Gen {
   }
   void need_inv() {
     if (inv_fresh) return;
-    line("T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);");
+    // folded copy: 1/dir and the per-axis reciprocals the axis-aligned planes divide by (exact under
+    // the folded copy's ray bound, see rcp_ref / div_ref in device/rt_body.h)
+    line(fold && fast_div ? "dir_rcp(T, r);" : "T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);");
     inv_fresh = true;
+  }
+  // folded copy: a plane whose normal is +-(unit axis) has denominator +-r.d.<axis>; returns the axis
+  // (0..2, -1 otherwise) and whether the denominator is negated
+  static int axis_den(const E &den, bool *neg) {
+    const char *names[3] = {"r.d.x", "r.d.y", "r.d.z"};
+    for (int a = 0; a < 3; ++a) {
+      if (den.s == names[a]) { *neg = false; return a; }
+      if (den.s == std::string("(-") + names[a] + ")") { *neg = true; return a; }
+    }
+    return -1;
+  }
+  bool needs_dir(const uint32_t *w) const {   // visit reads T.inv / T.rcp
+    if (w[W_KIND] == K_BVH) return true;
+    if (!fold || (w[W_KIND] != K_QUAD && w[W_KIND] != K_TRIANGLE)) return false;
+    const E d[3] = {{"r.d.x"}, {"r.d.y"}, {"r.d.z"}};
+    bool neg;
+    return share_rcp && axis_den(dotc(w + W_NORMAL, d, true), &neg) >= 0;
   }
   bool boxes_later() const { return visits < boxes_after.size() && boxes_after[visits] > 0; }
 
@@ -114,7 +137,23 @@ struct Gen {
     // t for every lane (a tiny denominator only yields inf/NaN there), one branch for both tests
     // dd - x with dd = +-0 is -x up to the sign of a zero t (which fails the tmin test either way)
     const std::string num = is_zero(w[W_D]) ? "(-" + val(non) + ")" : "(" + f(w[W_D]) + " - " + val(non) + ")";
-    line("const float t" + k + " = " + num + " / den" + k + ";");
+    // num / den without div_scale / div_fixup: in every lane where t matters (|den| >= 1e-8, t in
+    // [tmin, tmax]) the folded copy's bounds (|o|, |d| <= 1e9, constants <= 1e6) put |den| in
+    // [2^-27, 2^52] and |num| in [2^-37, 2^52], where that sequence is a/b bit for bit; elsewhere a
+    // tiny numerator still gives |t| < tmin and a tiny denominator fails the |den| test, so every
+    // predicate is unchanged.  Axis-aligned planes reuse the direction's reciprocal (x/(-b) == -(x/b)).
+    bool neg = false;
+    const int ax_d = axis_den(den, &neg);
+    const char *axn[3] = {"x", "y", "z"};
+    if (ax_d >= 0 && share_rcp) {
+      need_inv();
+      line("const float t" + k + " = " + (neg ? "-" : "") + "div_ref(" + num + ", r.d." + axn[ax_d] + ", T.rcp." +
+           axn[ax_d] + ");");
+    } else if (fast_div) {
+      line("const float t" + k + " = div_ref(" + num + ", den" + k + ", rcp_ref(den" + k + "));");
+    } else {
+      line("const float t" + k + " = " + num + " / den" + k + ";");
+    }
     line("if ((fabsf(den" + k + ") >= kDenomEps) & (kTmin <= t" + k + ") & (t" + k + " <= T.tmax)) {");
     indent += 2;
     line("const f3 p" + k + " = mk(r.o.x + r.d.x * t" + k + ", r.o.y + r.d.y * t" + k + ", r.o.z + r.d.z * t" + k + ");");
@@ -182,7 +221,7 @@ struct Gen {
     const uint32_t *w = node(i);
     if (collect) {
       if (kinds.size() <= visits) kinds.resize(visits + 1, 0);
-      kinds[visits] = static_cast<uint8_t>(w[W_KIND]);
+      kinds[visits] = needs_dir(w) ? 1 : 0;
     }
     const std::string xf = (in_t || in_r) ? "true" : "false";
     switch (w[W_KIND]) {
@@ -300,8 +339,9 @@ bool foldable(const SceneImage &img) {
 bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
                            bool *folded) {
   fold = fold && foldable(img);
-  Gen g1{img, max_visits};   // pass 1: pre-order visit kinds (for the lazy 1/dir)
+  Gen g1{img, max_visits};   // pass 1: pre-order visits that read 1/dir (for the lazy 1/dir)
   g1.collect = true;
+  g1.fold = fold;
   g1.walk(img.root, false, false, 0);
   if (!g1.ok) {
     if (visits) *visits = g1.visits;
@@ -310,7 +350,7 @@ bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold
   Gen g{img, max_visits};
   g.boxes_after.assign(g1.kinds.size() + 1, 0);
   for (size_t k = g1.kinds.size(); k-- > 0;)
-    g.boxes_after[k] = g.boxes_after[k + 1] + (k + 1 < g1.kinds.size() && g1.kinds[k + 1] == K_BVH ? 1u : 0u);
+    g.boxes_after[k] = g.boxes_after[k + 1] + (k + 1 < g1.kinds.size() && g1.kinds[k + 1] ? 1u : 0u);
   g.fold = fold;
   g.fold_uv = fold && !img.needs_uv;
   g.walk(img.root, false, false, 0);

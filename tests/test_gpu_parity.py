@@ -252,7 +252,7 @@ def test_capped_rejection_tries_agree(idx, tries, monkeypatch):
     monkeypatch.setenv("RT_DEFER_LANES", defer or "0")
     w, s = rt.build_scene(idx)
     cam, W, H = rt.camera_from_settings(s, 33, 19)
-    for force in (rt.RT_FLAG_FORCE_STATIC, rt.RT_FLAG_FORCE_LANE):
+    for force in (rt.RT_FLAG_FORCE_STATIC, rt.RT_FLAG_FORCE_LANE, rt.RT_FLAG_FORCE_PACKET):
         p = rt.make_params(s, W, H, spp=5, bounces=min(s.max_bounces, 50), flags=force | rt.RT_FLAG_COUNT)
         fb, st = gpu(w.scene(), cam, p)
         rc, ref, ost = oracle_render(w.scene(), cam, p)
