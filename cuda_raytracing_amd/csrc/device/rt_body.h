@@ -735,6 +735,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
 
   bool busy = false;                      // lane owns a pixel
+  bool hot = false;                       // the pixel is one of the first A.prio_ids handed out
+  bool raised = false;                    // wave-uniform: s_setprio raised
   int32_t pix = 0, sample = 0;
   uint32_t depth = 0;
   Rng rng{0, 0, 0, 0, 0, 0};
@@ -832,6 +834,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           pix = static_cast<int32_t>(lr * A.width + j);
           need = false;
           busy = true;
+          hot = id < A.prio_ids;
           if (A.probe_cost) {               // throwaway stream: the real ones are not consumed
             probe_tile = tile;
             probe_rounds = 0;
@@ -855,6 +858,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     const uint64_t lanes = __ballot(busy);
     if (lanes == 0) break;   // queue exhausted and every lane idle
+    // the slowest pixels bound the frame (a pixel's samples form one serial chain): waves holding
+    // pixels of the costliest tiles get issue priority over the waves that have slack
+    const bool want_raise = __ballot(busy && hot) != 0;
+    if (want_raise != raised) {
+      if (want_raise) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+      raised = want_raise;
+    }
     rounds++;
     busy_lane_rounds += static_cast<uint64_t>(__popcll(lanes));
     if (TRACE) {
@@ -891,6 +902,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       // lane needs a try, after try_cap tries, or once at most A.defer_lanes lanes are left (those
       // resume next round): the wave no longer runs the maximum of 64 geometric try counts.
       bool want = true;
+      // deferring only pays when the lanes that accepted outnumber the pending ones: a nearly empty
+      // wave (the tail of the frame) keeps trying rather than spending a round per try
+      const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(true)));
       for (uint32_t k = 0;;) {
         if (want) {
           float z = rng.sym();   // bound(-1, 1)
@@ -911,7 +925,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           if (acc) { ruv = mk(x, y, z); want = false; }
         }
         const uint64_t left = __ballot(want);
-        if (left == 0 || ++k == try_cap || static_cast<uint32_t>(__popcll(left)) <= A.defer_lanes) break;
+        const uint32_t nleft = static_cast<uint32_t>(__popcll(left));
+        if (left == 0 || ++k == try_cap || (nleft <= A.defer_lanes && 4 * nleft <= started)) break;
       }
       pending = want ? 1u : 0u;
     }

@@ -116,6 +116,8 @@ struct RenderArgs {
   uint32_t reverse_tiles;         // no order array: 1 = hand tiles out bottom row first
   uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
+  uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of
+                                  // the longest-first order) run their wave at raised issue priority
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the
                                   // wave still need a try (they resume next round; 0 = never early)
   uint32_t black_skip;            // every attenuation is finite (host-checked): a path ending in

@@ -153,6 +153,7 @@ struct rt_context {
   bool rc_lds_auto = true;                      // RT_RC_LDS_LEVELS given: exactly that many
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
+  int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
   uint32_t defer_lanes = 4;                     // RT_DEFER_LANES: end a round's rejection at <= this many lanes
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
   bool shade_spec = true;                       // RT_JIT_SHADE=0: run-time kernels keep every material
@@ -232,6 +233,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_LANE")) c->lane_jit = e[0] != '0';
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+  if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
@@ -455,6 +457,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), s) != hipSuccess)
       return RT_ERR_HIP;
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
+    const int pt = c->prio_tiles >= 0 ? c->prio_tiles : 0;
+    a.prio_ids = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(pt) * 64u, a.n_ids));
   }
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)

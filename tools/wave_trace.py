@@ -49,3 +49,8 @@ xcc = (rec[:, 3] >> np.uint64(32)).astype(np.int64)
 for x in np.unique(xcc):
     m = xcc == x
     print(f"  xcc {x}: waves {m.sum()} end p50 {100 * np.median(end[m] / span):.1f}% max {100 * end[m].max() / span:.1f}%")
+top = np.argsort(-end)[:5]
+for w in top:
+    r = rec[w]
+    print(f"straggler wave {w}: end {100 * end[w] / span:.1f}% rounds {int(r[4])} busy-lane-rounds {int(r[5])} "
+          f"tiles {int(r[2])} us/round {(end[w] - start[w]) / 100 / max(int(r[4]), 1):.2f}")
