@@ -51,7 +51,7 @@ OPS_PER_SAMPLE_FIXED = 30                 # camera ray generation
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
-TRAV_NAMES = {0: "lane-dfs", 1: "wave-packet-dfs", 2: "scene-specialised"}
+TRAV_NAMES = {0: "lane-dfs", 1: "wave-packet-dfs", 2: "scene-specialised", 3: "verified-sah"}
 
 
 def log(*a):
@@ -270,7 +270,8 @@ def main():
                 "pixels_per_gpu": rows * W,
                 "frames_in_flight": nf,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
-                "kernel": "rt_static_render (hipRTC)" if cst.traversal == rt.RT_TRAV_STATIC else "render_kernel",
+                "kernel": {rt.RT_TRAV_STATIC: "rt_static_render (hipRTC)", rt.RT_TRAV_ACCEL: "rt_accel_render (hipRTC)"}.get(
+                    cst.traversal, "rt_lane_render (hipRTC)"),
             },
             "kernel_ms": {"render_isolated": round(iso.render_ms, 3), "seed_isolated": round(iso.init_ms, 3),
                           "schedule_isolated": round(iso.sched_ms, 3),

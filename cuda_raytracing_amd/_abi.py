@@ -29,7 +29,8 @@ RT_FLAG_GLOBAL_SCENE = 0x2
 RT_FLAG_NO_JIT = 0x4
 RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET, RT_FLAG_FORCE_STATIC = 0x8, 0x10, 0x20
 RT_FLAG_NO_FOLD = 0x40
-RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC = 0, 1, 2
+RT_FLAG_FORCE_ACCEL, RT_FLAG_NO_ACCEL = 0x80, 0x100
+RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_TRAV_ACCEL = 0, 1, 2, 3
 
 CNT_NAMES = [
     "visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate",
@@ -93,6 +94,7 @@ class Stats(C.Structure):
         ("traversal", C.c_int32), ("jit_visits", C.c_int32),
         ("sched_ms", C.c_double),
         ("folded", C.c_int32), ("fold_rerenders", C.c_int32),
+        ("accel_spheres", C.c_int32), ("accel_depth", C.c_int32),
     ]
 
     def counter_dict(self):
@@ -163,7 +165,7 @@ def host_lib():
 
 HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_timing",
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
-               "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device"]
+               "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build"]
 
 
 def _bind_single_hip_runtime():
@@ -205,6 +207,7 @@ def hip_lib():
              C.c_uint64)
         _sig(L.rt_context_note, C.c_char_p, P)
         _sig(L.rt_tonemap_device, C.c_int, P, C.c_uint64, P, P)
+        _sig(L.rt_accel_build, C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
         _hip = L
     return _hip
 

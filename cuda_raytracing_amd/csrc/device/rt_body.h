@@ -603,6 +603,153 @@ struct LaneTraceK {
 using LaneTrace = LaneTraceK<0x7fu>;
 
 // ---------------------------------------------------------------------------------------------
+// traversal policy 4: verified sphere traversal (all-sphere worlds, sphere_accel.cpp)
+// ---------------------------------------------------------------------------------------------
+// For a world of spheres the record hit() returns does not depend on the order of the tests, only on
+// which spheres the walk reaches: a sphere contributes its first root in (tmin, inf) and is accepted
+// iff that root is below the running tmax (:1100-1110), so the closest-so-far only ever shrinks to
+// the minimum over the reached spheres — unless two spheres yield the same root bitwise (then the
+// first one tested wins).  The reference reaches a sphere iff the slab test (:990-1025) of every BVH
+// ancestor passes with the tmax of that moment, which is >= the final t*.  Hence, for a ray, if
+//   (1) a walk of ANY tree over the same spheres reaches every sphere the reference could accept
+//       (conservative boxes, below), and finds the minimum t* at sphere P with no other root == t*,
+//   (2) the reference's tests of P's BVH ancestors pass with tmax = t* (then with any larger tmax);
+//       ancestors contain P's deepest ancestor box B exactly (unions of boxes, :571-580) and the
+//       rounded slab values are monotone in the box bounds, so it suffices that the computed hit point
+//       lies inside B with a margin that absorbs the rounding of the slab test,
+// then the reference returns P's record at t*, and the record computed here from P and the same ray is
+// bit-identical.  Rays failing (1)'s preconditions, with a tie, or failing (2) are re-traced with the
+// reference's own walk (LaneTraceK).  Conservative boxes: a computed root can lie off the sphere —
+// disc = b^2 - 4ac cancels — but within sqrt(r^2 + 32u|oc|^2) of the centre (u = 2^-24), i.e. within
+// r + 2^-9 |oc| (|oc| <= |o|_1 + M, M bounding |centre| + r over a subtree); boxes are padded by that
+// (slab test on the padded box, NaN-tolerant), so no sphere the reference could accept is culled.
+__device__ __forceinline__ bool accel_box(const Trav &T, const Ray &r, float x0, float x1, float y0, float y1, float z0,
+                                          float z1, float pad, float *tnear) {
+  float a = (x0 - pad - r.o.x) * T.inv.x, c = (x1 + pad - r.o.x) * T.inv.x;
+  float t0 = fmaxf(kTmin, fminf(a, c)), t1 = fminf(T.tmax, fmaxf(a, c));
+  a = (y0 - pad - r.o.y) * T.inv.y; c = (y1 + pad - r.o.y) * T.inv.y;
+  t0 = fmaxf(t0, fminf(a, c)); t1 = fminf(t1, fmaxf(a, c));
+  a = (z0 - pad - r.o.z) * T.inv.z; c = (z1 + pad - r.o.z) * T.inv.z;
+  t0 = fmaxf(t0, fminf(a, c)); t1 = fminf(t1, fmaxf(a, c));
+  *tnear = t0;
+  return !(t1 < t0);
+}
+
+// sphere branch of hit() with the record commit of sphere_hit<UV>; also reports a root equal to tmax
+template <bool UV>
+__device__ __forceinline__ bool sphere_hit_tie(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
+                                               float inv_rad, bool &tie) {
+  f3 center = line_at(c0, r.time, mv);
+  f3 oc = sub(center, r.o);
+  float a = dot(r.d, r.d);
+  float b = -2.0f * dot(r.d, oc);
+  float c = dot(oc, oc) - rad2;
+  float disc = b * b - 4 * a * c;
+  if (!(disc >= 0)) return false;
+  float sq = sqrtf(disc);
+  float root = (-b - sq) / (2.0f * a);
+  tie |= root == T.tmax;
+  if (kTmin >= root || root >= T.tmax) {
+    root = (-b + sq) / (2.0f * a);
+    tie |= root == T.tmax;
+  }
+  if (!(kTmin < root && root < T.tmax)) return false;
+  h.t = root;
+  h.p = line_at(r.o, root, r.d);
+  h.mat = mat;
+  f3 outward = scale(inv_rad, sub(h.p, center));
+  if (UV) {
+    const float pi = 3.1415926535897932385f;
+    float theta = rt_acosf(-outward.y);
+    float phi = rt_atan2f(-outward.z, outward.x) + pi;
+    h.u = phi / (2 * pi);
+    h.v = theta / pi;
+  }
+  h.fd = dot(r.d, outward);
+  h.n = outward;
+  T.tmax = h.t;
+  T.result = true;
+  return true;
+}
+
+template <uint32_t KM>
+struct AccelTraceK {
+  template <bool LDS, bool COUNT, bool UV>
+  __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t lanes,
+                                             uint32_t lane, uint16_t *stk, Trav &T, Ray &r, Hit &h, Visits &vc) {
+    if (!busy) return;
+    trav_reset(T, r);
+    const float ao = fabsf(r.o.x) + fabsf(r.o.y) + fabsf(r.o.z);
+    const float dmin = fminf(fminf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+    const float dmax = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+    // bounded, finite rays with no tiny direction component (finite 1/dir); the counting variant
+    // walks the reference tree so that the op model counts the reference's visits
+    const bool nice = !COUNT && (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f);
+    bool tie = false;
+    uint32_t best = 0;
+    const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
+    const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.accel_prims);
+    if (nice) {
+      const float kap = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24)
+      const float pad_o = kap * ao;
+      auto leaf = [&](uint32_t ref) {
+        const uint32_t first = ref & 0xffffffu, cnt = ((ref >> 24) & 0x7fu) + 1u;
+        for (uint32_t k = 0; k < cnt; ++k) {
+          const uint4 p0 = P[(first + k) * 4], p1 = P[(first + k) * 4 + 1], p2 = P[(first + k) * 4 + 2];
+          if (sphere_hit_tie<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
+                                 asf(p1.z), asf(p1.w), tie))
+            best = first + k;
+        }
+      };
+      uint32_t node = A.accel_root;
+      int sp = 0;
+      for (;;) {
+        const uint4 q0 = N[node * 4], q1 = N[node * 4 + 1], q2 = N[node * 4 + 2], q3 = N[node * 4 + 3];
+        float n0, n1;
+        bool h0 = accel_box(T, r, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y),
+                            pad_o + kap * asf(q3.z), &n0);
+        bool h1 = accel_box(T, r, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w),
+                            pad_o + kap * asf(q3.w), &n1);
+        const bool near0 = n0 <= n1;
+        const uint32_t rn = near0 ? q3.x : q3.y, rf = near0 ? q3.y : q3.x;
+        bool hn = near0 ? h0 : h1, hf = near0 ? h1 : h0;
+        if (hn && (rn & kAccelLeaf)) { leaf(rn); hn = false; }
+        if (hf && (rf & kAccelLeaf)) { leaf(rf); hf = false; }
+        if (hn && hf) {
+          stk[sp * 64] = static_cast<uint16_t>(rf);
+          ++sp;
+          node = rn;
+        } else if (hn | hf) {
+          node = hn ? rn : rf;
+        } else {
+          if (sp == 0) break;
+          --sp;
+          node = stk[sp * 64];
+        }
+      }
+    }
+    bool need_ref = !nice || tie;
+    if (nice && T.result) {
+      // (2): the hit point inside P's deepest reference BVH ancestor box with a margin of 2^-16 of
+      // the magnitudes the slab test rounds (|o|, |p|, |t d| per axis; ~100x its worst-case error)
+      const uint4 b0 = P[best * 4 + 2], b1 = P[best * 4 + 3];
+      const float bx0 = asf(b0.z), bx1 = asf(b0.w), by0 = asf(b1.x), by1 = asf(b1.y), bz0 = asf(b1.z), bz1 = asf(b1.w);
+      const float m = 1.52587890625e-05f;   // 2^-16
+      const float dx = m * (fabsf(r.o.x) + fabsf(h.p.x) + fabsf(h.t * r.d.x)) + 1.0e-30f;
+      const float dy = m * (fabsf(r.o.y) + fabsf(h.p.y) + fabsf(h.t * r.d.y)) + 1.0e-30f;
+      const float dz = m * (fabsf(r.o.z) + fabsf(h.p.z) + fabsf(h.t * r.d.z)) + 1.0e-30f;
+      const bool inside = (h.p.x - bx0 >= dx) & (bx1 - h.p.x >= dx) & (h.p.y - by0 >= dy) & (by1 - h.p.y >= dy) &
+                          (h.p.z - bz0 >= dz) & (bz1 - h.p.z >= dz);
+      need_ref |= !inside;
+    }
+    if (__ballot(need_ref) != 0) {   // rare: the reference walk for those lanes
+      asm volatile("" ::: "memory");
+      LaneTraceK<KM>::template run<LDS, COUNT, UV>(S, A, need_ref, lanes, lane, stk, T, r, h, vc);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
 // traversal policy 2: one DFS per wave with per-entry lane masks
 // ---------------------------------------------------------------------------------------------
 // The reference's DFS order is fixed by the scene, not by the ray: a hit BVH node pushes right then

@@ -30,6 +30,14 @@ enum : int {
   W_OFFSET = 2, W_SIN = 2, W_COS = 3, W_COUNT = 2,
 };
 
+// Verified sphere traversal (sphere_accel.cpp, AccelTraceK): a binned-SAH BVH2 over the spheres of
+// an all-sphere world.  Node = 16 words: child boxes (x0 x1 y0 y1 z0 z1) at 0 and 6, child refs at
+// 12/13 (kAccelLeaf | (count-1) << 24 | first prim, or a node index), per child at 14/15 an upper
+// bound M of |centre(t)| + radius over its spheres.  Prim = 16 words, in leaf order.
+constexpr int kAccelNodeWords = 16, kAccelPrimWords = 16;
+constexpr uint32_t kAccelLeaf = 0x80000000u;
+enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
+
 // materials (raytracing.cu:78-99): 8 words; kinds == RTR_MAT_* (rt_ref_layout.h)
 constexpr int kMatWords = 8;
 enum : int { M_KIND = 0, M_TEX = 1, M_ALBEDO = 2, M_FUZZ = 5, M_IOR = 6 };
@@ -116,6 +124,7 @@ struct RenderArgs {
   uint32_t reverse_tiles;         // no order array: 1 = hand tiles out bottom row first
   uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
+  uint32_t accel_nodes, accel_prims, accel_root;   // verified sphere traversal (word offsets, root node)
   uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of
                                   // the longest-first order) run their wave at raised issue priority
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the

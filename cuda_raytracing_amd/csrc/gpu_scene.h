@@ -26,6 +26,14 @@ struct SceneImage {
   bool has_noise = false;
 };
 
+// SAH BVH over the spheres of an all-sphere world (sphere_accel.cpp; word layout: device/rt_layout.h)
+struct SphereAccel {
+  std::vector<uint32_t> node_words, prim_words;
+  uint32_t root = 0, depth = 0, spheres = 0;
+};
+// false (with a reason) when the world is not an all-sphere BVH/group tree with >= min_spheres spheres
+bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel *out, std::string *why);
+
 // Returns RT_OK or RT_ERR_SCENE / RT_ERR_UNSUPPORTED.
 int compile_scene(const void *scene /* const rt_scene* */, SceneImage *out);
 

@@ -67,6 +67,7 @@ static_assert(rt::CNT_BOUNCES == RT_CNT_BOUNCES && rt::CNT_SHADES == RT_CNT_SHAD
 static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::K_GROUP == RTR_OBJ_GROUP, "kinds");
 
 constexpr int kLptMinSpp = 16;
+constexpr uint32_t kAccelMinSpheres = 64;   // smaller all-sphere worlds: the scene-specialised walk
 constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr uint32_t kRcLdsMaxLevels = 16;   // fold only when every ray provably stays below this
@@ -133,6 +134,10 @@ struct rt_context {
   int device = 0;
   int cu_count = 0;
   SceneImage img;
+  // verified sphere traversal (RT_TRAV_ACCEL): SAH tree words appended to the device scene image
+  rt::SphereAccel accel;
+  bool accel_ok = false;
+  uint32_t accel_nodes = 0, accel_prims = 0;   // word offsets in the device image
   DevBuf scene, jump, rng, rc, work, counters, wave_trace, tile_cost, tile_order;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
@@ -175,6 +180,27 @@ struct rt_context {
 extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]) {
+  if (!scene || !info) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  int st = rt::compile_scene(scene, &img);
+  if (st != RT_OK) return st;
+  rt::SphereAccel a;
+  std::string why;
+  if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
+  info[0] = a.root;
+  info[1] = a.depth;
+  info[2] = a.spheres;
+  info[3] = static_cast<uint32_t>(a.node_words.size());
+  const uint64_t n = a.node_words.size() + a.prim_words.size();
+  if (words) {
+    if (cap < n) return RT_ERR_INVALID_ARG;
+    std::memcpy(words, a.node_words.data(), a.node_words.size() * 4);
+    std::memcpy(words + a.node_words.size(), a.prim_words.data(), a.prim_words.size() * 4);
+  }
+  return RT_OK;
+}
 
 const char *rt_status_string(int s) {
   switch (s) {
@@ -238,6 +264,18 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
+  std::vector<uint32_t> dev_words = c->img.words;
+  {
+    const char *e = std::getenv("RT_ACCEL");
+    std::string why;
+    if (!(e && e[0] == '0') && rt::build_sphere_accel(c->img, kAccelMinSpheres, &c->accel, &why)) {
+      c->accel_ok = true;
+      c->accel_nodes = static_cast<uint32_t>(dev_words.size());
+      dev_words.insert(dev_words.end(), c->accel.node_words.begin(), c->accel.node_words.end());
+      c->accel_prims = static_cast<uint32_t>(dev_words.size());
+      dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
+    }
+  }
   if (c->img.stack_need > 512) { delete c; return RT_ERR_STACK; }
   c->black_skip = attenuations_finite(c->img);
   if (const char *e = std::getenv("RT_BLACK_SKIP")) c->black_skip = c->black_skip && e[0] != '0';
@@ -246,8 +284,8 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_context_destroy(c); return RT_ERR_HIP; }
   c->cu_count = prop.multiProcessorCount;
   const std::vector<uint32_t> &J = rt::xorwow_jump_tables();
-  bool ok = c->scene.ensure(c->img.words.size() * 4) == hipSuccess &&
-            hipMemcpy(c->scene.p, c->img.words.data(), c->img.words.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
+  bool ok = c->scene.ensure(dev_words.size() * 4) == hipSuccess &&
+            hipMemcpy(c->scene.p, dev_words.data(), dev_words.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
             c->jump.ensure(J.size() * 4) == hipSuccess &&
             hipMemcpy(c->jump.p, J.data(), J.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
             c->work.ensure(64) == hipSuccess &&
@@ -288,7 +326,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   const uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
   uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
   uint32_t rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
-  size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * c->img.stack_need * 64 * 2;
+  // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
+  const uint32_t stack_cap = std::max(c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u);
+  size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
   c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
@@ -301,7 +341,10 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   if (p->flags & RT_FLAG_FORCE_LANE) trav = RT_TRAV_LANE;
   else if (p->flags & RT_FLAG_FORCE_PACKET) trav = RT_TRAV_PACKET;
   else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
-  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC)) trav = RT_TRAV_LANE;
+  else if (p->flags & RT_FLAG_FORCE_ACCEL) trav = RT_TRAV_ACCEL;
+  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC || trav == RT_TRAV_ACCEL)) trav = RT_TRAV_LANE;
+  const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
+  if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = RT_TRAV_LANE;
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
   hipFunction_t jit_fn = nullptr, jit_probe = nullptr;
   bool jit_lane = false;
@@ -317,6 +360,18 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
       jit_probe = jk.probe;
       c->jit_visits = jk.visits;
       trav = RT_TRAV_STATIC;
+    } else {
+      c->jit_why = why;
+      trav = accel_allowed ? RT_TRAV_ACCEL : RT_TRAV_LANE;
+    }
+  }
+  if (trav == RT_TRAV_ACCEL) {
+    rt::JitKernels jk;
+    std::string why;
+    if (rt::jit_accel_kernels(c->img, c->variant | trace_bit, &jk, &why)) {
+      jit_fn = c->counted ? jk.render_count : jk.render;
+      jit_probe = jk.probe;
+      jit_lane = true;   // per-lane stacks
     } else {
       c->jit_why = why;
       trav = RT_TRAV_LANE;
@@ -386,7 +441,10 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.off_pixels = c->img.off_pixels;
   a.pixel_words = static_cast<uint32_t>(c->img.words.size()) - c->img.off_pixels;
   a.root = c->img.root;
-  a.stack_cap = c->img.stack_need;
+  a.stack_cap = stack_cap;
+  a.accel_nodes = c->accel_nodes;
+  a.accel_prims = c->accel_prims;
+  a.accel_root = c->accel.root;
   a.rc_lds_word = scene_lds_words;
   a.rc_lds_levels = rc_levels;
   a.stack_lds_word = scene_lds_words + rc_lds_words;
@@ -481,6 +539,8 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->jit_visits = static_cast<int32_t>(c->jit_visits);
   st->folded = c->used_fold ? 1 : 0;
   st->fold_rerenders = static_cast<int32_t>(c->fold_violations);
+  st->accel_spheres = c->accel_ok ? static_cast<int32_t>(c->accel.spheres) : 0;
+  st->accel_depth = c->accel_ok ? static_cast<int32_t>(c->accel.depth) : 0;
   if (!c->rendered) return RT_OK;
   DeviceGuard g(c->device);
   if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;

@@ -214,6 +214,26 @@ std::string jit_lane_source(const SceneImage &img, int variant) {
   return src;
 }
 
+std::string jit_accel_source(const SceneImage &img, int variant) {
+  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | (15 << kVarMatShift) | (15 << kVarTexShift));
+  const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u>";
+  std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render(RenderArgs A) {\n  render_body<" +
+         std::to_string(v) + ", " + at + ">(A);\n}\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render_count(RenderArgs A) {\n  render_body<" +
+         std::to_string(v | kVarCount) + ", " + at + ">(A);\n}\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_probe(RenderArgs A) {\n  render_body<" +
+         std::to_string(v) + ", " + at + ">(A);\n}\n";
+  src += "}  // namespace rt\n";
+  return src;
+}
+
+bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
+  out->visits = 0;
+  out->folded = false;
+  return build_module(jit_accel_source(img, variant), "rt_accel", out, why);
+}
+
 bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;

@@ -33,6 +33,9 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
 // kind dispatch of trav_step keeps only those branches).  Same contract as jit_kernels.
 bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
 std::string jit_lane_source(const SceneImage &img, int variant);
+// Verified sphere traversal kernels (AccelTraceK over the scene's node kinds for the fallback walk).
+bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
+std::string jit_accel_source(const SceneImage &img, int variant);
 uint32_t scene_kinds(const SceneImage &img);
 // material / texture kinds present, as variant bits (kVarMatShift / kVarTexShift)
 int scene_shading_bits(const SceneImage &img);

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* status codes */
 #define RT_OK                 0
@@ -80,13 +80,17 @@ typedef struct rt_params {
 #define RT_FLAG_NO_JIT      0x4u   /* never use the scene-specialised (hipRTC) traversal */
 #define RT_FLAG_FORCE_LANE   0x8u  /* force RT_TRAV_LANE   (A/B and parity tests; default: auto) */
 #define RT_FLAG_FORCE_PACKET 0x10u /* force RT_TRAV_PACKET (falls back to LANE if the stack is too deep) */
-#define RT_FLAG_FORCE_STATIC 0x20u /* force RT_TRAV_STATIC (falls back to LANE over the visit budget) */
+#define RT_FLAG_FORCE_STATIC 0x20u /* force RT_TRAV_STATIC (over the visit budget: ACCEL if eligible, else LANE) */
 #define RT_FLAG_NO_FOLD      0x40u /* RT_TRAV_STATIC without exact constant folding of primitive tests */
+#define RT_FLAG_FORCE_ACCEL  0x80u /* force RT_TRAV_ACCEL (falls back to LANE when the world is not all spheres) */
+#define RT_FLAG_NO_ACCEL     0x100u /* never use RT_TRAV_ACCEL */
 
 /* traversal policies (rt_stats.traversal) */
 #define RT_TRAV_LANE   0   /* per-lane DFS over an LDS stack (any scene) */
 #define RT_TRAV_PACKET 1   /* one DFS per wave with per-entry lane masks */
 #define RT_TRAV_STATIC 2   /* the scene's DFS expanded to straight-line code, compiled with hipRTC */
+#define RT_TRAV_ACCEL  3   /* all-sphere worlds: SAH tree walk, verified against the reference tree per ray
+                              (rays it cannot verify take the reference walk; bit-identical records) */
 
 /* rt_stats.counters[] slots (filled only with RT_FLAG_COUNT) */
 enum {
@@ -115,6 +119,8 @@ typedef struct rt_stats {
   double sched_ms;         /* longest-first schedule: probe paths + tile sort, before the render kernel */
   int32_t folded;          /* 1 if the specialised traversal used exactly folded primitive tests */
   int32_t fold_rerenders;  /* frames re-rendered unfolded after a ray left the host's bound (expect 0) */
+  int32_t accel_spheres;   /* spheres in the verified traversal's tree (RT_TRAV_ACCEL), else 0 */
+  int32_t accel_depth;     /* depth of that tree */
 } rt_stats;
 
 /* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of
@@ -146,6 +152,11 @@ int rt_tonemap_device(const float *rgb_device, uint64_t pixels, uint8_t *out_dev
  * rt_static_compile: compiles that source for `arch` (e.g. "gfx950"); the compiler log goes to log. */
 int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint64_t cap, uint32_t *visits);
 int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *arch, char *log, uint64_t cap);
+/* Diagnostics for the verified sphere traversal (no device needed): builds the SAH tree of an
+ * all-sphere world.  info = {root node, depth, spheres, node words}; words (if non-null, cap words)
+ * receives the node words then the prim words (layout: device/rt_layout.h kAccel*).
+ * RT_ERR_UNSUPPORTED when the world is not eligible. */
+int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
 /* Last fallback reason of a context (why RT_TRAV_STATIC was not used); "" if none. */
 const char *rt_context_note(const rt_context *ctx);
 

@@ -1,0 +1,112 @@
+"""Host-side checks of the verified sphere traversal's SAH tree (sphere_accel.cpp), no GPU needed.
+
+The kernel-side argument (device/rt_body.h, AccelTraceK) needs: every sphere of the world exactly once
+in the tree, every child box containing its spheres over the motion, M bounding |centre| + radius, and
+per sphere the box of its deepest BVH ancestor in the REFERENCE tree.  These are checked here on the
+catalog scenes the policy applies to; scenes with other primitives must be rejected.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import cuda_raytracing_amd as rt
+
+LEAF = 0x80000000
+
+
+def f(u):
+    return np.asarray(u, np.uint32).view(np.float32)
+
+
+def reference_spheres(sc):
+    """sphere record -> deepest BVH ancestor box (x0 x1 y0 y1 z0 z1), walking the reference records
+    (rtr_hittable, include/rt_ref_layout.h: 120 B, union at byte 8)."""
+    import ctypes as C
+    raw = np.frombuffer(C.string_at(sc.hittables, 120 * sc.hittable_count), np.uint8).reshape(-1, 120)
+    refs = np.ctypeslib.as_array(sc.refs, shape=(sc.ref_count,))
+    kind = raw[:, 0:4].copy().view(np.uint32)[:, 0]
+    out = {}
+    stack = [(int(refs[sc.root]), None)]
+    while stack:
+        i, parent = stack.pop()
+        if kind[i] == 1:   # BVH: u16 left/right WorldRefs, then the box
+            l, r = (int(refs[x]) for x in raw[i, 8:12].copy().view(np.uint16))
+            box = tuple(float(x) for x in raw[i, 12:36].copy().view(np.float32))
+            stack.append((l, box))
+            if r != l:
+                stack.append((r, box))
+        elif kind[i] == 0:
+            assert i not in out
+            out[i] = parent
+        elif kind[i] == 6:   # group: u16 first, count (u64) at union offset 40
+            first = int(raw[i, 8:10].copy().view(np.uint16)[0])
+            count = int(raw[i, 48:56].copy().view(np.uint64)[0])
+            for k in range(count):
+                stack.append(((first + k) & 0xffff, parent))
+        else:
+            return None
+    return out
+
+
+@pytest.mark.parametrize("idx", [2, rt.RT_SCENE_RANDOM_10K])
+def test_tree_covers_every_sphere_once(idx):
+    w, _ = rt.build_scene(idx)
+    sc = w.scene()
+    res = rt.accel_build(sc)
+    assert res is not None
+    info, nodes, prims = res
+    nodes = nodes.reshape(-1, 16)
+    prims = prims.reshape(-1, 16)
+    assert info["spheres"] == len(prims) and not (info["root"] & LEAF)
+    seen = np.zeros(len(prims), np.int32)
+    depth_max = 0
+    stack = [(info["root"], 1)]
+    while stack:
+        node, d = stack.pop()
+        depth_max = max(depth_max, d)
+        q = nodes[node]
+        for c in range(2):
+            box = f(q[6 * c: 6 * c + 6])
+            ref = int(q[12 + c])
+            m = float(f(q[14 + c]))
+            if ref & LEAF:
+                first, cnt = ref & 0xffffff, ((ref >> 24) & 0x7f) + 1
+                for k in range(first, first + cnt):
+                    seen[k] += 1
+                    p = prims[k]
+                    c0, mv = f(p[0:3]).astype(np.float64), f(p[3:6]).astype(np.float64)
+                    rad = np.sqrt(np.float64(f(p[6])))
+                    lo = np.minimum(c0, c0 + mv) - rad
+                    hi = np.maximum(c0, c0 + mv) + rad
+                    assert np.all(box[0::2] <= lo) and np.all(box[1::2] >= hi), (node, c, k)
+                    assert m >= np.linalg.norm(c0) + np.linalg.norm(mv) + rad - 1e-3
+            else:
+                cb = nodes[ref]
+                for cc in range(2):   # the child's boxes lie inside this box
+                    inner = f(cb[6 * cc: 6 * cc + 6])
+                    assert np.all(box[0::2] <= inner[0::2]) and np.all(box[1::2] >= inner[1::2])
+                stack.append((ref, d + 1))
+    assert np.all(seen == 1)
+    assert depth_max <= info["depth"] + 1
+
+
+@pytest.mark.parametrize("idx", [2, rt.RT_SCENE_RANDOM_10K])
+def test_verification_boxes_are_reference_ancestors(idx):
+    w, _ = rt.build_scene(idx)
+    sc = w.scene()
+    _, _, prims = rt.accel_build(sc)
+    prims = prims.reshape(-1, 16)
+    ref = reference_spheres(sc)
+    assert ref is not None and len(ref) == len(prims)
+    for p in prims:
+        node = int(p[9])
+        want = ref[node]
+        got = tuple(float(x) for x in f(p[10:16]))
+        assert want is not None and got == want, node
+
+
+@pytest.mark.parametrize("idx", [0, 1, 17])
+def test_other_worlds_are_not_eligible(idx):
+    w, _ = rt.build_scene(idx)
+    assert rt.accel_build(w.scene()) is None

@@ -209,7 +209,7 @@ def test_auto_policy_and_fallback():
     w, s = rt.build_scene(rt.RT_SCENE_RANDOM_10K)
     cam, W, H = rt.camera_from_settings(s, 16, 9)
     fb, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4, flags=rt.RT_FLAG_FORCE_STATIC))
-    assert st.traversal == rt.RT_TRAV_LANE
+    assert st.traversal == rt.RT_TRAV_ACCEL and st.accel_spheres > 10000
     rc, ref, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=1, bounces=4))
     assert np.array_equal(bits(fb), bits(ref))
 
@@ -312,3 +312,26 @@ def test_image_texture_scene_vs_oracle():
         p.flags = force
         fb, _ = gpu(w.scene(), cam, p)
         assert np.array_equal(bits(fb), bits(ref)), force
+
+
+@pytest.mark.parametrize("idx,W,H,spp", [(2, 64, 36, 4), (20, 64, 36, 4), (20, 160, 90, 6), (2, 128, 72, 8)])
+def test_verified_sphere_traversal_matches_oracle(idx, W, H, spp):
+    # SAH tree walk + per-ray proof against the reference tree (fallback to the reference walk)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL)
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_ACCEL and st.accel_spheres > 0
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("idx,W,H,spp,b", [(20, 480, 270, 16, 16), (2, 480, 270, 16, 50)])
+def test_verified_sphere_traversal_matches_reference_walk_large(idx, W, H, spp, b):
+    # millions of rays: the verified walk against the reference walk on the GPU (itself oracle-exact)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    a, sa = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_ACCEL))
+    c, sc = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_LANE))
+    assert sa.traversal == rt.RT_TRAV_ACCEL and sc.traversal == rt.RT_TRAV_LANE
+    assert np.array_equal(bits(a), bits(c))
