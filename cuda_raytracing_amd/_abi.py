@@ -95,6 +95,7 @@ class Stats(C.Structure):
         ("sched_ms", C.c_double),
         ("folded", C.c_int32), ("fold_rerenders", C.c_int32),
         ("accel_spheres", C.c_int32), ("accel_depth", C.c_int32),
+        ("accel_fallbacks", C.c_uint32), ("pad_", C.c_uint32),
     ]
 
     def counter_dict(self):

@@ -623,14 +623,17 @@ using LaneTrace = LaneTraceK<0x7fu>;
 // disc = b^2 - 4ac cancels — but within sqrt(r^2 + 32u|oc|^2) of the centre (u = 2^-24), i.e. within
 // r + 2^-9 |oc| (|oc| <= |o|_1 + M, M bounding |centre| + r over a subtree); boxes are padded by that
 // (slab test on the padded box, NaN-tolerant), so no sphere the reference could accept is culled.
-__device__ __forceinline__ bool accel_box(const Trav &T, const Ray &r, float x0, float x1, float y0, float y1, float z0,
-                                          float z1, float pad, float *tnear) {
-  float a = (x0 - pad - r.o.x) * T.inv.x, c = (x1 + pad - r.o.x) * T.inv.x;
-  float t0 = fmaxf(kTmin, fminf(a, c)), t1 = fminf(T.tmax, fmaxf(a, c));
-  a = (y0 - pad - r.o.y) * T.inv.y; c = (y1 + pad - r.o.y) * T.inv.y;
-  t0 = fmaxf(t0, fminf(a, c)); t1 = fminf(t1, fmaxf(a, c));
-  a = (z0 - pad - r.o.z) * T.inv.z; c = (z1 + pad - r.o.z) * T.inv.z;
-  t0 = fmaxf(t0, fminf(a, c)); t1 = fminf(t1, fmaxf(a, c));
+// The box arrives padded by the subtree's share kAccelKappa * M; the ray's share kAccelKappa * |o|_1
+// is added in t (pinv = that pad * |1/d| per axis).  Slab values by fma with oinv = o * (1/d): this
+// test only has to be conservative, and its rounding (~u |o| in space) is far inside the padding.
+__device__ __forceinline__ bool accel_box(const Trav &T, f3 oinv, f3 pinv, float x0, float x1, float y0, float y1,
+                                          float z0, float z1, float *tnear) {
+  float a = __builtin_fmaf(x0, T.inv.x, -oinv.x), c = __builtin_fmaf(x1, T.inv.x, -oinv.x);
+  float t0 = fmaxf(kTmin, fminf(a, c) - pinv.x), t1 = fminf(T.tmax, fmaxf(a, c) + pinv.x);
+  a = __builtin_fmaf(y0, T.inv.y, -oinv.y); c = __builtin_fmaf(y1, T.inv.y, -oinv.y);
+  t0 = fmaxf(t0, fminf(a, c) - pinv.y); t1 = fminf(t1, fmaxf(a, c) + pinv.y);
+  a = __builtin_fmaf(z0, T.inv.z, -oinv.z); c = __builtin_fmaf(z1, T.inv.z, -oinv.z);
+  t0 = fmaxf(t0, fminf(a, c) - pinv.z); t1 = fminf(t1, fmaxf(a, c) + pinv.z);
   *tnear = t0;
   return !(t1 < t0);
 }
@@ -690,8 +693,9 @@ struct AccelTraceK {
     const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
     const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.accel_prims);
     if (nice) {
-      const float kap = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24)
-      const float pad_o = kap * ao;
+      const float pad_o = kAccelKappa * ao;
+      const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
+      const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
       auto leaf = [&](uint32_t ref) {
         const uint32_t first = ref & 0xffffffu, cnt = ((ref >> 24) & 0x7fu) + 1u;
         for (uint32_t k = 0; k < cnt; ++k) {
@@ -706,10 +710,8 @@ struct AccelTraceK {
       for (;;) {
         const uint4 q0 = N[node * 4], q1 = N[node * 4 + 1], q2 = N[node * 4 + 2], q3 = N[node * 4 + 3];
         float n0, n1;
-        bool h0 = accel_box(T, r, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y),
-                            pad_o + kap * asf(q3.z), &n0);
-        bool h1 = accel_box(T, r, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w),
-                            pad_o + kap * asf(q3.w), &n1);
+        bool h0 = accel_box(T, oinv, pinv, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), &n0);
+        bool h1 = accel_box(T, oinv, pinv, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w), &n1);
         const bool near0 = n0 <= n1;
         const uint32_t rn = near0 ? q3.x : q3.y, rf = near0 ? q3.y : q3.x;
         bool hn = near0 ? h0 : h1, hf = near0 ? h1 : h0;
@@ -730,11 +732,12 @@ struct AccelTraceK {
     }
     bool need_ref = !nice || tie;
     if (nice && T.result) {
-      // (2): the hit point inside P's deepest reference BVH ancestor box with a margin of 2^-16 of
-      // the magnitudes the slab test rounds (|o|, |p|, |t d| per axis; ~100x its worst-case error)
+      // (2): the hit point inside P's deepest reference BVH ancestor box with a margin of 2^-19 of
+      // the magnitudes the slab test and the hit point round (|o|, |p|, |t d| per axis): the
+      // reference's slab values err by <= 3u |x - o| and p by <= 2u (|o| + |t d|), u = 2^-24
       const uint4 b0 = P[best * 4 + 2], b1 = P[best * 4 + 3];
       const float bx0 = asf(b0.z), bx1 = asf(b0.w), by0 = asf(b1.x), by1 = asf(b1.y), bz0 = asf(b1.z), bz1 = asf(b1.w);
-      const float m = 1.52587890625e-05f;   // 2^-16
+      const float m = 1.9073486328125e-06f;   // 2^-19
       const float dx = m * (fabsf(r.o.x) + fabsf(h.p.x) + fabsf(h.t * r.d.x)) + 1.0e-30f;
       const float dy = m * (fabsf(r.o.y) + fabsf(h.p.y) + fabsf(h.t * r.d.y)) + 1.0e-30f;
       const float dz = m * (fabsf(r.o.z) + fabsf(h.p.z) + fabsf(h.t * r.d.z)) + 1.0e-30f;
@@ -742,8 +745,10 @@ struct AccelTraceK {
                           (h.p.z - bz0 >= dz) & (bz1 - h.p.z >= dz);
       need_ref |= !inside;
     }
-    if (__ballot(need_ref) != 0) {   // rare: the reference walk for those lanes
+    const uint64_t fb = __ballot(need_ref);
+    if (fb != 0) {   // rare: the reference walk for those lanes
       asm volatile("" ::: "memory");
+      if (!COUNT && lane == static_cast<uint32_t>(__builtin_ctzll(fb))) atomicAdd(A.accel_fallbacks, static_cast<uint32_t>(__popcll(fb)));
       LaneTraceK<KM>::template run<LDS, COUNT, UV>(S, A, need_ref, lanes, lane, stk, T, r, h, vc);
     }
   }

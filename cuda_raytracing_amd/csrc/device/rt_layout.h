@@ -36,6 +36,7 @@ enum : int {
 // bound M of |centre(t)| + radius over its spheres.  Prim = 16 words, in leaf order.
 constexpr int kAccelNodeWords = 16, kAccelPrimWords = 16;
 constexpr uint32_t kAccelLeaf = 0x80000000u;
+constexpr float kAccelKappa = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24): cone padding per unit of |oc|
 enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
 
 // materials (raytracing.cu:78-99): 8 words; kinds == RTR_MAT_* (rt_ref_layout.h)
@@ -125,6 +126,7 @@ struct RenderArgs {
   uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
   uint32_t accel_nodes, accel_prims, accel_root;   // verified sphere traversal (word offsets, root node)
+  uint32_t *accel_fallbacks;      // rays the verified traversal handed to the reference walk (diagnostic)
   uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of
                                   // the longest-first order) run their wave at raised issue priority
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the

@@ -445,6 +445,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.accel_nodes = c->accel_nodes;
   a.accel_prims = c->accel_prims;
   a.accel_root = c->accel.root;
+  a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
   a.rc_lds_word = scene_lds_words;
   a.rc_lds_levels = rc_levels;
   a.stack_lds_word = scene_lds_words + rc_lds_words;
@@ -508,6 +509,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     pa.work = static_cast<uint32_t *>(c->work.p) + 8;
     pa.wave_trace = nullptr;
     pa.fold_violation = static_cast<uint32_t *>(c->work.p) + 14;   // probe rays: flag ignored
+    pa.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 13;  // probe rays: not reported
     const hipError_t pe = jit_probe ? rt::jit_launch(jit_probe, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                     : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
                                                         c->lds_bytes, s);
@@ -562,6 +564,9 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   if (hipEventElapsedTime(&a, c->ev[0], c->ev[1]) != hipSuccess) return RT_ERR_HIP;
   if (hipEventElapsedTime(&b, c->ev[1], c->ev[3]) != hipSuccess) return RT_ERR_HIP;
   if (hipEventElapsedTime(&d, c->ev[3], c->ev[2]) != hipSuccess) return RT_ERR_HIP;
+  if (c->used_traversal == RT_TRAV_ACCEL &&
+      hipMemcpy(&st->accel_fallbacks, static_cast<uint32_t *>(c->work.p) + 12, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return RT_ERR_HIP;
   st->init_ms = a;
   st->sched_ms = b;
   st->render_ms = d;

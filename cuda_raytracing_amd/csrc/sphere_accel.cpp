@@ -12,6 +12,7 @@
 // sphere is reached once (a span-1 leaf names it twice from one parent, :858-859: still one sphere).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -65,8 +66,10 @@ struct Builder {
   uint32_t max_depth = 0;
 
   static constexpr int kBins = 16;
-  static constexpr uint32_t kMaxLeaf = 4;
-  static constexpr double kTravCost = 1.0, kIsectCost = 1.5;
+  // SAH constants (A/B knobs RT_ACCEL_LEAF = max spheres per leaf, RT_ACCEL_ISECT = sphere test cost
+  // relative to a node visit)
+  uint32_t kMaxLeaf = 4;
+  double kTravCost = 1.0, kIsectCost = 1.5;
 
   // returns the child reference; fills its box and M
   uint32_t build(uint32_t b, uint32_t e, uint32_t depth, Box *box_out, double *m_out) {
@@ -147,11 +150,15 @@ struct Builder {
     const uint32_t r = build(mid, e, depth + 1, &rb, &rm);
     uint32_t *w = &nodes[static_cast<size_t>(idx) * kAccelNodeWords];
     const Box *cbx[2] = {&lb, &rb};
+    const double mm[2] = {lm, rm};
     for (int c = 0; c < 2; ++c) {
+      // stored pre-padded by the subtree's share of the cone padding, kAccelKappa * M (the ray's
+      // share, kAccelKappa * |o|_1, is applied in t by the kernel)
+      const double pad = static_cast<double>(kAccelKappa) * mm[c];
       uint32_t *o = w + 6 * c;
-      o[0] = fb(down(cbx[c]->lo[0])); o[1] = fb(up(cbx[c]->hi[0]));
-      o[2] = fb(down(cbx[c]->lo[1])); o[3] = fb(up(cbx[c]->hi[1]));
-      o[4] = fb(down(cbx[c]->lo[2])); o[5] = fb(up(cbx[c]->hi[2]));
+      o[0] = fb(down(cbx[c]->lo[0] - pad)); o[1] = fb(up(cbx[c]->hi[0] + pad));
+      o[2] = fb(down(cbx[c]->lo[1] - pad)); o[3] = fb(up(cbx[c]->hi[1] + pad));
+      o[4] = fb(down(cbx[c]->lo[2] - pad)); o[5] = fb(up(cbx[c]->hi[2] + pad));
     }
     w[12] = l;
     w[13] = r;
@@ -234,6 +241,8 @@ bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel
   if (prims.size() < min_spheres) { if (why) *why = "too few spheres"; return false; }
   if (prims.size() >= (1u << 24)) { if (why) *why = "too many spheres"; return false; }
   Builder bd;
+  if (const char *e = std::getenv("RT_ACCEL_LEAF")) bd.kMaxLeaf = static_cast<uint32_t>(std::max(1, std::min(64, std::atoi(e))));
+  if (const char *e = std::getenv("RT_ACCEL_ISECT")) bd.kIsectCost = std::max(0.05, std::atof(e));
   bd.prims = std::move(prims);
   Box rb;
   double rm;

@@ -121,6 +121,8 @@ typedef struct rt_stats {
   int32_t fold_rerenders;  /* frames re-rendered unfolded after a ray left the host's bound (expect 0) */
   int32_t accel_spheres;   /* spheres in the verified traversal's tree (RT_TRAV_ACCEL), else 0 */
   int32_t accel_depth;     /* depth of that tree */
+  uint32_t accel_fallbacks; /* rays of the last render the verified traversal re-traced with the reference walk */
+  uint32_t pad_;
 } rt_stats;
 
 /* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of
