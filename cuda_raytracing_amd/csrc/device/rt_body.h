@@ -11,6 +11,10 @@
 #pragma once
 #include "rt_layout.h"
 
+#ifndef RT_UNWIND_BATCH
+#define RT_UNWIND_BATCH 8   // HBM colour-stack levels loaded per batch in the deep-path unwind
+#endif
+
 namespace rt {
 
 // [scene image (LDS variant)] [colour-stack levels 0..rc_lds_levels-1] [per-lane traversal stacks]
@@ -866,6 +870,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   constexpr bool LDS = (F & kVarLds) != 0, COUNT = (F & kVarCount) != 0;
   constexpr bool NOISE = (F & kVarNoise) != 0, UV = (F & kVarUv) != 0;
   constexpr bool TRACE = (F & kVarTrace) != 0;   // per-wave timeline into A.wave_trace (diagnostics)
+  constexpr bool DEEP = (F & kVarDeep) != 0;     // batched unwind of HBM colour-stack levels
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
   Mem<LDS> S{A.scene};
@@ -1174,9 +1179,31 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         res = mk(0.0f, 0.0f, 0.0f);
         depth = 0;
       }
-      for (int32_t k = static_cast<int32_t>(depth) - 1; k >= 0; --k) {      // :1362-1368
+      // :1362-1368.  Levels past the LDS ones live in HBM/L2: their loads are issued kUnwindBatch at a
+      // time ahead of the multiply chain (one memory latency per batch, not per level — a deep path
+      // otherwise holds its whole wave for hundreds of cycles per level)
+      int32_t k = static_cast<int32_t>(depth) - 1;
+      const int32_t kl = static_cast<int32_t>(A.rc_lds_levels);
+      while (DEEP && k >= kl) {
+        constexpr int kUnwindBatch = RT_UNWIND_BATCH;
+        f3 at[kUnwindBatch];
+#pragma unroll
+        for (int i = 0; i < kUnwindBatch; ++i) {
+          if (k - i >= kl) {
+            const float *slot = A.rc + (static_cast<size_t>(k - i) * 3) * A.threads + gtid;
+            at[i] = mk(slot[0], slot[A.threads], slot[2 * static_cast<size_t>(A.threads)]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < kUnwindBatch; ++i) {
+          if (k - i >= kl) res = mk(at[i].x * res.x + 0.0f, at[i].y * res.y + 0.0f, at[i].z * res.z + 0.0f);
+        }
+        k -= kUnwindBatch;
+        if (k < kl) k = kl - 1;   // continue with the deepest LDS level
+      }
+      for (; k >= 0; --k) {
         f3 at;
-        if (static_cast<uint32_t>(k) < A.rc_lds_levels) {
+        if (DEEP || k < kl) {
           const float *slot = rc_l + k * 192;
           at = mk(slot[0], slot[64], slot[128]);
         } else {

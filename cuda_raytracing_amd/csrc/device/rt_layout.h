@@ -77,6 +77,10 @@ enum : int { kVarLds = 1, kVarCount = 2, kVarNoise = 4, kVarUv = 8, kVarPacket =
 // run-time compiled kernels also carry the material kinds (bits 6..9, bit MAT_*) and texture kinds
 // (bits 10..13, bit T_*) present in the scene; 0 in a field means "all" (the offline kernels)
 constexpr int kVarMatShift = 6, kVarTexShift = 10;
+// run-time compiled kernels for deep paths (max_bounces > kDeepBounces): colour-stack levels in HBM are
+// unwound with batched loads (costs registers, so shallow renders keep the plain loop)
+constexpr int kVarDeep = 1 << 14;
+constexpr int kDeepBounces = 16;
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling

@@ -70,6 +70,7 @@ constexpr int kLptMinSpp = 16;
 constexpr uint32_t kAccelMinSpheres = 64;   // smaller all-sphere worlds: the scene-specialised walk
 constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
+constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr uint32_t kRcLdsMaxLevels = 16;   // fold only when every ray provably stays below this
 
 // Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
@@ -333,7 +334,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
-  const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0);
+  const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
+                        (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0);
   // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
   // at most jit_budget node visits (every catalog scene but the large random ones), else the per-lane
   // DFS.  The wave-packet DFS is kept as an explicit option (fastest on tiny all-sphere scenes).
@@ -404,7 +406,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     const size_t fixed = static_cast<size_t>(scene_lds_words) * 4 + stack_bytes;
     const size_t level_bytes = static_cast<size_t>(rt::kWavesPerBlock) * 3 * 64 * 4;
     if (per_block > fixed) {
-      const uint32_t fit = static_cast<uint32_t>((per_block - fixed) / level_bytes);
+      // keep 1 KiB per block in reserve: resident blocks whose LDS sums to within ~1% of 160 KiB were
+      // measured NOT to be co-resident on gfx950 (3 x 53808 B: a third of the blocks started late)
+      const uint32_t fit = per_block > fixed + kLdsReserve ? static_cast<uint32_t>((per_block - fixed - kLdsReserve) / level_bytes) : 0u;
       const uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
       if (lv > rc_levels) {
         const size_t lds2 = fixed + lv * level_bytes;

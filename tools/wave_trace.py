@@ -52,5 +52,8 @@ for x in np.unique(xcc):
 top = np.argsort(-end)[:5]
 for w in top:
     r = rec[w]
+    ph = r[6:11].astype(np.float64)
     print(f"straggler wave {w}: end {100 * end[w] / span:.1f}% rounds {int(r[4])} busy-lane-rounds {int(r[5])} "
-          f"tiles {int(r[2])} us/round {(end[w] - start[w]) / 100 / max(int(r[4]), 1):.2f}")
+          f"tiles {int(r[2])} us/round {(end[w] - start[w]) / 100 / max(int(r[4]), 1):.2f} phases (cycles/round): "
+          + " ".join(f"{n} {v / max(int(r[4]), 1):.0f}" for n, v in
+                     zip(("refill", "trace", "unwind+cam", "mat", "rej"), ph)))
