@@ -335,3 +335,17 @@ def test_verified_sphere_traversal_matches_reference_walk_large(idx, W, H, spp, 
     c, sc = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_LANE))
     assert sa.traversal == rt.RT_TRAV_ACCEL and sc.traversal == rt.RT_TRAV_LANE
     assert np.array_equal(bits(a), bits(c))
+
+
+@pytest.mark.parametrize("idx,W,H,spp,b", [(0, 480, 270, 16, 16), (1, 320, 320, 8, 50), (17, 480, 270, 8, 50),
+                                          (16, 400, 400, 8, 50)])
+def test_static_fast_paths_match_reference_walk_large(idx, W, H, spp, b):
+    # millions of rays: the folded straight-line kernel (exact folding, division without
+    # div_scale/div_fixup, shared reciprocals, deferred rejection, deep-path unwind) against the
+    # plain per-lane reference walk, which is itself bit-exact against the oracle at small sizes
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    a, sa = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_STATIC))
+    c, sc = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_LANE | rt.RT_FLAG_NO_JIT))
+    assert sa.traversal == rt.RT_TRAV_STATIC and sa.folded == 1 and sc.traversal == rt.RT_TRAV_LANE
+    assert np.array_equal(bits(a), bits(c))
