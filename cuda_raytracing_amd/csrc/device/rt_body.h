@@ -333,6 +333,10 @@ struct Trav {
   int tc, yc;      // translation / y-rotation cleanup counters
   uint32_t was_last;   // 0/1 in a VGPR (a bool becomes per-join SALU lane-mask merges)
   bool result;
+  // verified traversal paused at the end of a round (resumed next round, shading skipped meanwhile)
+  uint32_t active;     // 1 = walk in progress
+  uint32_t anode, abest, atie;
+  int asp;
 };
 
 __device__ __forceinline__ void trav_reset(Trav &T, const Ray &r) {
@@ -592,16 +596,33 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
   T.sp = sp;
 }
 
-template <uint32_t KM>
+// PAUSE: the walk may stop at the end of a round with its state kept in T and the LDS stack (as in
+// AccelTraceK: the round's walk ends once at most A.defer_trace lanes, <= 1/4 of the starters, are
+// still walking after A.trace_min_iters steps); the walk resumes next round with shading skipped.
+template <uint32_t KM, bool PAUSE = false>
 struct LaneTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t, uint32_t,
                                              uint16_t *stk, Trav &T, Ray &r, Hit &h, Visits &vc) {
     if (!busy) return;
-    trav_reset(T, r);
-    stk[0] = static_cast<uint16_t>(A.root);
-    T.sp = 1;
-    while (T.sp > 0) trav_step<LDS, COUNT, UV, KM>(S, T, r, h, stk, vc);
+    if (!PAUSE || !T.active) {
+      trav_reset(T, r);
+      stk[0] = static_cast<uint16_t>(A.root);
+      T.sp = 1;
+    }
+    if (!PAUSE) {
+      while (T.sp > 0) trav_step<LDS, COUNT, UV, KM>(S, T, r, h, stk, vc);
+      return;
+    }
+    const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(true)));
+    for (uint32_t it = 1;; ++it) {
+      if (T.sp > 0) trav_step<LDS, COUNT, UV, KM>(S, T, r, h, stk, vc);
+      const uint64_t left = __ballot(T.sp > 0);
+      if (left == 0) break;
+      const uint32_t nl = static_cast<uint32_t>(__popcll(left));
+      if (it >= A.trace_min_iters && nl <= A.defer_trace && 4 * nl <= started) break;
+    }
+    T.active = T.sp > 0 ? 1u : 0u;
   }
 };
 using LaneTrace = LaneTraceK<0x7fu>;
@@ -685,17 +706,19 @@ struct AccelTraceK {
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t lanes,
                                              uint32_t lane, uint16_t *stk, Trav &T, Ray &r, Hit &h, Visits &vc) {
     if (!busy) return;
-    trav_reset(T, r);
+    const bool resume = T.active != 0;
+    if (!resume) trav_reset(T, r);
     const float ao = fabsf(r.o.x) + fabsf(r.o.y) + fabsf(r.o.z);
     const float dmin = fminf(fminf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
     const float dmax = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
     // bounded, finite rays with no tiny direction component (finite 1/dir); the counting variant
     // walks the reference tree so that the op model counts the reference's visits
     const bool nice = !COUNT && (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f);
-    bool tie = false;
-    uint32_t best = 0;
+    bool tie = resume && T.atie != 0;
+    uint32_t best = resume ? T.abest : 0u;
     const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
     const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.accel_prims);
+    bool walking = nice;
     if (nice) {
       const float pad_o = kAccelKappa * ao;
       const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
@@ -709,9 +732,16 @@ struct AccelTraceK {
             best = first + k;
         }
       };
-      uint32_t node = A.accel_root;
-      int sp = 0;
-      for (;;) {
+      uint32_t node = resume ? T.anode : A.accel_root;
+      int sp = resume ? T.asp : 0;
+      // Wave-uniform loop, one node per walking lane per step.  Rays differ wildly in length (the
+      // horizon of a sphere field vs a close hit), so instead of every lane waiting for the longest
+      // walk, the round's walk ends once few lanes remain (A.defer_trace, after A.trace_min_iters
+      // steps); those lanes keep node, stack and best hit and resume next round, skipping shading
+      // meanwhile.  A walk's steps and order are unchanged, so the record is the same.
+      const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(walking)));
+      for (uint32_t it = 1;; ++it) {
+        if (walking) {
         const uint4 q0 = N[node * 4], q1 = N[node * 4 + 1], q2 = N[node * 4 + 2], q3 = N[node * 4 + 3];
         float n0, n1;
         bool h0 = accel_box(T, oinv, pinv, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), &n0);
@@ -727,13 +757,24 @@ struct AccelTraceK {
           node = rn;
         } else if (hn | hf) {
           node = hn ? rn : rf;
+        } else if (sp == 0) {
+          walking = false;
         } else {
-          if (sp == 0) break;
           --sp;
           node = stk[sp * 64];
         }
+        }
+        const uint64_t left = __ballot(walking);
+        if (left == 0) break;
+        const uint32_t nl = static_cast<uint32_t>(__popcll(left));
+        if (it >= A.trace_min_iters && nl <= A.defer_trace && 4 * nl <= started) break;
+      }
+      if (walking) {   // paused: resume next round
+        T.active = 1; T.anode = node; T.asp = sp; T.abest = best; T.atie = tie ? 1u : 0u;
+        return;
       }
     }
+    T.active = 0;
     bool need_ref = !nice || tie;
     if (nice && T.result) {
       // (2): the hit point inside P's deepest reference BVH ancestor box with a margin of 2^-19 of
@@ -901,7 +942,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
   f3 sum = mk(0, 0, 0);
   Trav T;
-  T.inv = mk(0, 0, 0); T.rcp = mk(0, 0, 0); T.tmax = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = 0; T.result = false;
+  T.inv = mk(0, 0, 0); T.rcp = mk(0, 0, 0); T.tmax = 0; T.active = 0; T.anode = 0; T.abest = 0; T.atie = 0; T.asp = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = 0; T.result = false;
   Hit h;
   h.u = 0; h.v = 0; h.t = 0; h.fd = 0; h.mat = 0; h.p = mk(0, 0, 0); h.n = mk(0, 0, 0);
   Visits vc{};
@@ -1034,6 +1075,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     // ---- trace one path segment per busy lane (hit(), :1340) ----
     const bool tracing = busy && !pending;   // a lane still resuming its rejection keeps its hit
     Trace::template run<LDS, COUNT, UV>(S, A, tracing, __ballot(tracing), lane, stk, T, ray, h, vc);
+    if (T.active) continue;                   // walk paused (verified traversal): resumes next round
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       ph_trace += t - t_mark;

@@ -131,6 +131,8 @@ struct RenderArgs {
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
   uint32_t accel_nodes, accel_prims, accel_root;   // verified sphere traversal (word offsets, root node)
   uint32_t *accel_fallbacks;      // rays the verified traversal handed to the reference walk (diagnostic)
+  uint32_t defer_trace;           // verified traversal: the round's walk stops once at most this many
+  uint32_t trace_min_iters;       // lanes (and <= 1/4 of the starters) still walk, after this many steps
   uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of
                                   // the longest-first order) run their wave at raised issue priority
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the

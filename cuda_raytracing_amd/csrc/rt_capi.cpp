@@ -161,6 +161,7 @@ struct rt_context {
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
   uint32_t defer_lanes = 4;                     // RT_DEFER_LANES: end a round's rejection at <= this many lanes
+  uint32_t defer_trace = 16, trace_min_iters = 16;  // RT_DEFER_TRACE, RT_TRACE_MIN (paused per-lane walks)
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
   bool shade_spec = true;                       // RT_JIT_SHADE=0: run-time kernels keep every material
   uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
@@ -261,6 +262,8 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
+  if (const char *e = std::getenv("RT_DEFER_TRACE")) c->defer_trace = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+  if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
@@ -479,6 +482,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.black_skip = c->black_skip ? 1u : 0u;
   a.max_tries = c->max_tries;
   a.defer_lanes = c->defer_lanes;
+  a.defer_trace = c->defer_trace;
+  a.trace_min_iters = c->trace_min_iters;
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;

@@ -202,7 +202,7 @@ uint32_t scene_kinds(const SceneImage &img) {
 
 std::string jit_lane_source(const SceneImage &img, int variant) {
   const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | (15 << kVarMatShift) | (15 << kVarTexShift));
-  const std::string lt = "LaneTraceK<" + std::to_string(scene_kinds(img)) + "u>";
+  const std::string lt = "LaneTraceK<" + std::to_string(scene_kinds(img)) + "u, true>";   // pausable walk
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v) + ", " + lt + ">(A);\n}\n";
