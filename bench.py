@@ -133,7 +133,7 @@ def load_traffic(workload: str):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", type=int, default=0)
     ap.add_argument("--width", type=int, default=1920)

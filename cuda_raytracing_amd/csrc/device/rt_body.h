@@ -14,6 +14,9 @@
 #ifndef RT_UNWIND_BATCH
 #define RT_UNWIND_BATCH 8   // HBM colour-stack levels loaded per batch in the deep-path unwind
 #endif
+#ifndef RT_UNWIND_LDS
+#define RT_UNWIND_LDS 3     // LDS colour-stack levels loaded per batch in the unwind
+#endif
 
 namespace rt {
 
@@ -296,6 +299,9 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
         const uint32_t tb = A.off_perlin + t0.y * kPerlinWords;
         float accum = 0.0f, weight = 1.0f;
         f3 q = p;
+        // unrolled: the octaves' table reads are independent, so their LDS latencies overlap (a
+        // path trapped between the noise spheres runs alone on its SIMD at the end of the frame)
+#pragma unroll
         for (int oct = 0; oct < 7; ++oct) {
           accum += weight * perlin_noise(S, tb, q);
           weight *= 0.5f;
@@ -1243,16 +1249,26 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         k -= kUnwindBatch;
         if (k < kl) k = kl - 1;   // continue with the deepest LDS level
       }
-      for (; k >= 0; --k) {
-        f3 at;
-        if (DEEP || k < kl) {
-          const float *slot = rc_l + k * 192;
-          at = mk(slot[0], slot[64], slot[128]);
-        } else {
-          const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
-          at = mk(slot[0], slot[A.threads], slot[2 * static_cast<size_t>(A.threads)]);
+      for (; !DEEP && k >= kl; --k) {   // shallow kernels: HBM levels are rare, one at a time
+        const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
+        res = mk(slot[0] * res.x + 0.0f, slot[A.threads] * res.y + 0.0f, slot[2 * static_cast<size_t>(A.threads)] * res.z + 0.0f);
+      }
+      // LDS levels, RT_UNWIND_LDS at a time: the loads of a batch are issued together (one LDS latency
+      // per batch, not per level).  Levels below 0 read level 0 and multiply by 1.0f instead (exact).
+      // The "+ 0.0f" of each level only turns a -0 into +0 (an underflowed product stays +-0 in every
+      // later level) and sum = +0 + ... is never -0, so dropping it leaves the pixel bit-identical.
+      for (; k >= 0; k -= RT_UNWIND_LDS) {
+        f3 at[RT_UNWIND_LDS];
+#pragma unroll
+        for (int i = 0; i < RT_UNWIND_LDS; ++i) {
+          const float *slot = rc_l + max(k - i, 0) * 192;
+          at[i] = mk(slot[0], slot[64], slot[128]);
         }
-        res = mk(at.x * res.x + 0.0f, at.y * res.y + 0.0f, at.z * res.z + 0.0f);
+#pragma unroll
+        for (int i = 0; i < RT_UNWIND_LDS; ++i) {
+          if (k - i < 0) at[i] = mk(1.0f, 1.0f, 1.0f);
+          res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
+        }
       }
       sum = add(sum, res);
       sample++;

@@ -429,6 +429,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
   blocks = std::max<uint64_t>(1, std::min(blocks, needed));
   const uint32_t threads = static_cast<uint32_t>(blocks * rt::kBlock);
+  if (std::getenv("RT_DEBUG"))
+    std::fprintf(stderr, "[rt] launch: traversal %d, %d blocks/CU, %llu blocks, lds %zu B (scene %u words, colour-stack levels %u, stack cap %u)\n",
+                 trav, per_cu, static_cast<unsigned long long>(blocks), c->lds_bytes, scene_lds_words, rc_levels, stack_cap);
 
   if (c->rng.ensure(static_cast<size_t>(n) * 6 * 4) != hipSuccess) return RT_ERR_HIP;
   if (c->rc.ensure(static_cast<size_t>(mb) * 3 * threads * 4) != hipSuccess) return RT_ERR_HIP;
