@@ -71,6 +71,7 @@ constexpr uint32_t kAccelMinSpheres = 64;   // smaller all-sphere worlds: the sc
 constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
+constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr uint32_t kRcLdsMaxLevels = 16;   // fold only when every ray provably stays below this
 
 // Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
@@ -529,7 +530,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), s) != hipSuccess)
       return RT_ERR_HIP;
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
-    const int pt = c->prio_tiles >= 0 ? c->prio_tiles : 0;
+    const int pt = c->prio_tiles >= 0 ? c->prio_tiles : kPrioTiles;
     a.prio_ids = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(pt) * 64u, a.n_ids));
   }
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;

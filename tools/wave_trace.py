@@ -57,3 +57,12 @@ for w in top:
           f"tiles {int(r[2])} us/round {(end[w] - start[w]) / 100 / max(int(r[4]), 1):.2f} phases (cycles/round): "
           + " ".join(f"{n} {v / max(int(r[4]), 1):.0f}" for n, v in
                      zip(("refill", "trace", "unwind+cam", "mat", "rej"), ph)))
+# per dispatch rank: block b reaches its CU in round b // n_cu of the dispatch (n_cu = 256 blocks
+# per round on MI355X), so its waves are the (b // n_cu)-th oldest of their SIMDs
+wid = np.arange(len(rec))
+rank = (wid // 4) // 256
+for rk in np.unique(rank):
+    m = rank == rk
+    upr = (end[m] - start[m]) / 100 / np.maximum(rec[m, 4].astype(np.float64), 1)
+    print(f"  dispatch rank {rk}: waves {m.sum()} us/round mean {upr.mean():.2f} rounds mean {rec[m, 4].mean():.0f} "
+          f"tiles mean {tiles[m].mean():.2f} end p50 {100 * np.median(end[m] / span):.1f}% max {100 * end[m].max() / span:.1f}%")
