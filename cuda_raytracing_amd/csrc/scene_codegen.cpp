@@ -61,6 +61,10 @@ struct Gen {
   // cache it in T.inv.  Here it is (re)computed only before a box test that follows a direction change
   // (start, y-rotation enter/exit), instead of at every rotation — same values, fewer divisions.
   bool inv_fresh = false;
+  // per-axis reciprocals (T.rcp) of the current direction: a folded axis-aligned plane needs only its
+  // own, so after a rotation the planes refresh one axis each (3 ops) instead of the whole dir_rcp
+  // (three reciprocals, three 1/dir divisions and the exactness check); inv_fresh implies all three
+  bool rcp_fresh[3] = {false, false, false};
   // A/B knobs: RT_JIT_FASTDIV=0 keeps the compiler's division in the folded copy; RT_JIT_SHARE_RCP=0
   // gives every axis-aligned plane its own reciprocal instead of the direction's shared one
   bool fast_div = !(std::getenv("RT_JIT_FASTDIV") && std::getenv("RT_JIT_FASTDIV")[0] == '0');
@@ -80,6 +84,17 @@ struct Gen {
     // the folded copy's ray bound, see rcp_ref / div_ref in device/rt_body.h)
     line(fold && fast_div ? "dir_rcp(T, r);" : "T.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);");
     inv_fresh = true;
+    for (bool &b : rcp_fresh) b = fold && fast_div;
+  }
+  void need_rcp(int axis) {   // folded copy only (share_rcp): T.rcp.<axis> of the current direction
+    if (rcp_fresh[axis]) return;
+    const char *axn[3] = {"x", "y", "z"};
+    line(std::string("T.rcp.") + axn[axis] + " = rcp_ref(r.d." + axn[axis] + ");");
+    rcp_fresh[axis] = true;
+  }
+  void dir_changed() {
+    inv_fresh = false;
+    for (bool &b : rcp_fresh) b = false;
   }
   // folded copy: a plane whose normal is +-(unit axis) has denominator +-r.d.<axis>; returns the axis
   // (0..2, -1 otherwise) and whether the denominator is negated
@@ -146,7 +161,7 @@ struct Gen {
     const int ax_d = axis_den(den, &neg);
     const char *axn[3] = {"x", "y", "z"};
     if (ax_d >= 0 && share_rcp) {
-      need_inv();
+      need_rcp(ax_d);
       line("const float t" + k + " = " + (neg ? "-" : "") + "div_ref(" + num + ", r.d." + axn[ax_d] + ", T.rcp." +
            axn[ax_d] + ");");
     } else if (fast_div) {
@@ -295,11 +310,11 @@ struct Gen {
         if (in_r) { ok = false; return; }
         line("if (COUNT) vc.k[" + u(K_YROTATE) + "]++;");
         line("rotate_enter_dir(T, r, " + f(w[W_SIN]) + ", " + f(w[W_COS]) + ");   // node " + u(i));
-        inv_fresh = false;
+        dir_changed();
         walk(w[W_AUX], in_t, true, depth + 1);
         line("if (COUNT) vc.k[" + u(K_YROTATE) + "]++;");
         line("rotate_exit_dir(T, r, h, " + f(w[W_SIN]) + ", " + f(w[W_COS]) + ");");
-        inv_fresh = false;
+        dir_changed();
         break;
       case K_GROUP:
         line("if (COUNT) vc.k[" + u(K_GROUP) + "]++;");
