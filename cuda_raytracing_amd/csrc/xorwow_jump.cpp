@@ -52,12 +52,23 @@ void build() {
     std::memcpy(a.r[b], v, sizeof v);
   }
   for (int i = 0; i < 67; ++i) { square(a, t); a = t; }
-  g_tables.resize(static_cast<size_t>(kJumpPowers) * kJumpMatrixWords);
+  g_tables.resize(static_cast<size_t>(kJumpNibbleOffset) + kJumpNibbleWords);
   for (int k = 0; k < kJumpPowers; ++k) {
     std::memcpy(g_tables.data() + static_cast<size_t>(k) * kJumpMatrixWords, a.r, sizeof a.r);
     square(a, t);
     a = t;
   }
+  const uint32_t *p0 = g_tables.data();   // P_0, rows [b][word]
+  uint32_t *lo = g_tables.data() + kJumpNibbleOffset, *hi = lo + kJumpNibbles * 16 * 4;
+  for (int c = 0; c < kJumpNibbles; ++c)
+    for (int v = 0; v < 16; ++v) {
+      uint32_t r[5] = {0, 0, 0, 0, 0};
+      for (int i = 0; i < 4; ++i)
+        if ((v >> i) & 1)
+          for (int w = 0; w < 5; ++w) r[w] ^= p0[(4 * c + i) * 5 + w];
+      for (int w = 0; w < 4; ++w) lo[(c * 16 + v) * 4 + w] = r[w];
+      hi[c * 16 + v] = r[4];
+    }
 }
 
 }  // namespace

@@ -8,7 +8,12 @@ namespace rt {
 constexpr int kJumpPowers = 40;                 // subsequences < 2^40
 constexpr int kJumpMatrixWords = 160 * 5;       // rows[b][k]: image of unit vector e_b
 
-// P_k = A^(2^67 * 2^k), k in [0, kJumpPowers), concatenated (row-major [k][b][word]).
+// P_k = A^(2^67 * 2^k), k in [0, kJumpPowers), concatenated (row-major [k][b][word]), followed by
+// the nibble table of P_0 (the step to the next subsequence) at kJumpNibbleOffset: for input nibble c
+// (bits 4c..4c+3 of the 160-bit state) and value v, the XOR of P_0's rows for v's bits — words 0..3
+// as 640 uint4 [c * 16 + v], then word 4 as 640 u32.  P_0 x = XOR over c of table[c][nibble_c(x)].
+constexpr int kJumpNibbles = 40, kJumpNibbleWords = kJumpNibbles * 16 * 5;
+constexpr int kJumpNibbleOffset = kJumpPowers * kJumpMatrixWords;   // 16-B aligned (128 000 B)
 const std::vector<uint32_t> &xorwow_jump_tables();
 
 // Seeded state {d, x0..x4} for (seed, subsequence) — same as rocrand_init(seed, subsequence, 0).
