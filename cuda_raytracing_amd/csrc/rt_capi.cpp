@@ -72,7 +72,7 @@ constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
-constexpr uint32_t kRcLdsMaxLevels = 16;   // fold only when every ray provably stays below this
+constexpr uint32_t kRcLdsMaxLevels = 64;   // colour-stack levels kept in LDS at most
 
 // Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
 // precondition, scene_codegen.cpp).  Primary rays: camera centre + lens offset, directions to the
@@ -405,6 +405,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   }
   c->used_traversal = trav;
   int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes) : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
+  if (c->blocks_per_cu > 0) per_cu = std::min(c->blocks_per_cu, per_cu);   // fewer blocks: more LDS levels each
   if (c->rc_lds_auto) {
     // give the colour stack every LDS byte the resident blocks leave unused (deeper paths then never
     // touch HBM), without lowering residency
@@ -418,7 +419,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
       const uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
       if (lv > rc_levels) {
         const size_t lds2 = fixed + lv * level_bytes;
-        const int per_cu2 = jit_fn ? rt::jit_blocks_per_cu(jit_fn, lds2) : rt::render_blocks_per_cu(c->variant, lds2);
+        int per_cu2 = jit_fn ? rt::jit_blocks_per_cu(jit_fn, lds2) : rt::render_blocks_per_cu(c->variant, lds2);
+        if (c->blocks_per_cu > 0) per_cu2 = std::min(c->blocks_per_cu, per_cu2);
         if (per_cu2 >= per_cu) {
           rc_levels = lv;
           rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
