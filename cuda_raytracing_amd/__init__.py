@@ -306,6 +306,14 @@ def static_compile(scene: Scene, arch: str = "gfx950", max_visits: int = 256) ->
     return log.value.decode(errors="replace")
 
 
+def seed_states(seed: int, width: int, row_offset: int, row_stride: int, rows: int) -> np.ndarray:
+    """Device-seeded per-pixel XORWOW states [6, rows*width] (d, x0..x4) — rt_seed_states."""
+    out = np.empty((6, rows * width), dtype=np.uint32)
+    _check(_abi.hip_lib().rt_seed_states(seed, width, row_offset, row_stride, rows, out.ctypes.data_as(C.c_void_p)),
+           "rt_seed_states")
+    return out
+
+
 def tonemap(rgb: np.ndarray) -> np.ndarray:
     """raytracing.cu:1391-1395,1419-1433: sqrt gamma, clamp [0,0.999], x256 -> u8."""
     src = np.ascontiguousarray(rgb, dtype=np.float32)

@@ -678,4 +678,33 @@ int rt_tonemap_device(const float *rgb, uint64_t pixels, uint8_t *out, void *str
   return RT_OK;
 }
 
+int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out) {
+  if (!out || width <= 0 || rows <= 0 || row_offset < 0 || row_stride <= 0) return RT_ERR_INVALID_ARG;
+  const uint64_t n = static_cast<uint64_t>(rows) * static_cast<uint64_t>(width);
+  if (n > 0x7fffffffull) return RT_ERR_INVALID_ARG;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RT_ERR_NO_DEVICE;
+  const std::vector<uint32_t> &J = rt::xorwow_jump_tables();
+  DevBuf jump, states;
+  int rc = RT_OK;
+  if (jump.ensure(J.size() * 4) != hipSuccess || states.ensure(n * 6 * 4) != hipSuccess ||
+      hipMemcpy(jump.p, J.data(), J.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    rc = RT_ERR_HIP;
+  } else {
+    rt::SeedArgs sa{};
+    sa.jump = static_cast<const uint32_t *>(jump.p);
+    rt::xorwow_seed_base(seed, sa.base);
+    sa.width = width; sa.row_offset = row_offset; sa.row_stride = row_stride;
+    sa.n_pixels = static_cast<uint32_t>(n);
+    sa.per_thread = 16;
+    sa.rng = static_cast<uint32_t *>(states.p);
+    if (rt::launch_seed(sa, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out, states.p, n * 6 * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = RT_ERR_HIP;
+  }
+  jump.release();
+  states.release();
+  return rc;
+}
+
 const char *rt_context_note(const rt_context *c) { return c ? c->jit_why.c_str() : ""; }

@@ -349,3 +349,33 @@ def test_static_fast_paths_match_reference_walk_large(idx, W, H, spp, b):
     c, sc = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_LANE | rt.RT_FLAG_NO_JIT))
     assert sa.traversal == rt.RT_TRAV_STATIC and sa.folded == 1 and sc.traversal == rt.RT_TRAV_LANE
     assert np.array_equal(bits(a), bits(c))
+
+
+def _uniforms_from_states(st: np.ndarray, n: int) -> np.ndarray:
+    """rocrand_uniform draws of XORWOW states [6, m] (d, x0..x4): numpy restatement, float32."""
+    d, x0, x1, x2, x3, x4 = (st[k].astype(np.uint32).copy() for k in range(6))
+    out = np.empty((st.shape[1], n), dtype=np.float32)
+    inv = np.float32(2.0 ** -32)
+    for k in range(n):
+        t = x0 ^ (x0 >> np.uint32(2))
+        x0, x1, x2, x3 = x1, x2, x3, x4
+        x4 = (x4 ^ (x4 << np.uint32(4))) ^ (t ^ (t << np.uint32(1)))
+        d = d + np.uint32(362437)
+        out[:, k] = (d + x4).astype(np.float32) * inv + inv   # f*inv exact, one rounding of the sum
+    return out
+
+
+@pytest.mark.parametrize("width,rows,row_offset,row_stride", [(3840, 3, 2157, 1), (3840, 4, 1, 541),
+                                                             (1920, 2, 1078, 1), (2715, 3, 5, 509)])
+def test_device_seeding_matches_oracle_at_full_size(width, rows, row_offset, row_stride):
+    # init_gpu_data (:1591-1606) at BASELINE sizes: subsequence = global pixel index up to 8.3 M (4K);
+    # every pixel of the sampled rows vs the oracle's own rocRAND-equivalent seeding, 8 draws each
+    st = rt.seed_states(1234, width, row_offset, row_stride, rows)
+    got = _uniforms_from_states(st, 8)
+    L = _abi.oracle_lib()
+    ref = np.empty(8, dtype=np.float32)
+    for k in range(rows):
+        g0 = (row_offset + k * row_stride) * width
+        for j in list(range(0, width, 97)) + [width - 1]:
+            L.rt_oracle_uniforms(1234, g0 + j, ref.ctypes.data_as(C.c_void_p), 8)
+            assert np.array_equal(got[k * width + j].view(np.uint32), ref.view(np.uint32)), (k, j)
