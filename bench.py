@@ -217,10 +217,14 @@ def main():
             retire()
 
     run(max(args.warmup, 1) if nf > 1 else args.warmup)
-    # one isolated frame: the render kernel's own duration for the roofline (no overlap)
-    launch(0)
-    retire()
-    iso = stats[-1]
+    # isolated frames: the render kernel's own duration for the roofline (no overlap); the median
+    # of three, since one frame's tail varies by a few percent from run to run
+    isos = []
+    for _ in range(3):
+        launch(0)
+        retire()
+        isos.append(stats[-1])
+    iso = sorted(isos, key=lambda st: st.render_ms)[1]
     stats.clear()
     if world_size > 1:
         dist.barrier()
