@@ -379,3 +379,25 @@ def test_device_seeding_matches_oracle_at_full_size(width, rows, row_offset, row
         for j in list(range(0, width, 97)) + [width - 1]:
             L.rt_oracle_uniforms(1234, g0 + j, ref.ctypes.data_as(C.c_void_p), 8)
             assert np.array_equal(got[k * width + j].view(np.uint32), ref.view(np.uint32)), (k, j)
+
+
+@pytest.mark.parametrize("scene,args", [(0, ["s4", "b4", "w64", "h36"]), (17, ["s2", "b50", "w48", "h27"])])
+def test_cli_writes_the_oracle_ppm(scene, args, tmp_path):
+    # the reference's CLI surface (main.cu:29-131, `./raytracing 0 s4 b4` is BASELINE config 1) end to
+    # end on the GPU: catalog scene -> BVH -> camera -> rt_render -> settings.img_name as P6 bytes
+    import subprocess
+    from conftest import REPO
+    exe = REPO / "bin" / "raytracing"
+    assert exe.exists(), "bin/raytracing not built (make cli)"
+    r = subprocess.run([str(exe), str(scene), *args], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    w, s = rt.build_scene(scene)
+    opts = {a[0]: int(a[1:]) for a in args}
+    cam, W, H = rt.camera_from_settings(s, opts["w"], opts["h"])
+    p = rt.make_params(s, W, H, spp=opts["s"], bounces=opts["b"])
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    data = (tmp_path / s.img_name.decode()).read_bytes()
+    header = f"P6\n{W} {H}\n255\n".encode()
+    assert data.startswith(header)
+    assert data[len(header):] == rt.tonemap(ref).tobytes()
