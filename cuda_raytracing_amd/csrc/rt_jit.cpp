@@ -79,7 +79,7 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
   return true;
 }
 
-bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log, bool slp) {
+bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log) {
   hiprtcProgram prog;
   const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
   const char *hdr_names[] = {"rt_layout.h", "rt_body.h"};
@@ -87,14 +87,13 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
     if (log) *log = "hiprtcCreateProgram failed";
     return false;
   }
-  // Same numerics flags as the offline build.  slp: SLP vectorisation packs pairs of independent f32
-  // adds/muls/fmas into v_pk_*_f32 — two lane-ops per wave64 issue where a scalar f32 op takes one
-  // issue of 4 cycles (tools/valu_peak.hip), each half rounded as the scalar op (no contraction:
-  // bit-identical).  It costs ~10 VGPRs (scene 0: 72 -> 81, one wave less per SIMD) and still wins on
-  // the traversal-bound scene-specialised kernels (scene 0 -4 %, Cornell -2 %); the noise-texture
-  // and per-lane walk kernels keep it off.  RT_JIT_OPTS appends options (A/B experiments).
+  // Same numerics flags as the offline build.  SLP vectorisation is off: on this code it packs
+  // scalar f32 pairs into v_pk_* with extra moves, turns the planar inside-test into a <4 x i1>
+  // reduction, and its longer live ranges spill ~100 SGPRs (measured: -10% instructions, 86 -> 71
+  // VGPRs on scene 0; measured again in round 1: +30 % frame time).  RT_JIT_OPTS appends options (A/B
+  // experiments); hipRTC keeps the FIRST of two conflicting flags, so it cannot override these.
   std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                                "-fhip-fp32-correctly-rounded-divide-sqrt", slp ? "-fslp-vectorize" : "-fno-slp-vectorize"};
+                                "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
   for (const std::string &x : jit_extra_options()) o.push_back(x);
   std::vector<const char *> opts;
   for (const std::string &x : o) opts.push_back(x.c_str());
@@ -126,11 +125,11 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
 namespace {
 
 // Compile (or fetch) the module of `src` exporting <prefix>_render, <prefix>_render_count, <prefix>_probe.
-bool build_module(const std::string &src, const std::string &prefix, JitKernels *out, std::string *why, bool slp = false) {
+bool build_module(const std::string &src, const std::string &prefix, JitKernels *out, std::string *why) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const std::string arch = arch_of(dev);
-  std::string key = arch + "|" + std::to_string(dev) + (slp ? "|slp|" : "|");
+  std::string key = arch + "|" + std::to_string(dev) + "|";
   for (const std::string &x : jit_extra_options()) key += x + " ";
   key += "|" + src;
   std::lock_guard<std::mutex> lock(g_mu);
@@ -139,7 +138,7 @@ bool build_module(const std::string &src, const std::string &prefix, JitKernels 
     auto e = std::make_unique<Entry>();
     std::vector<char> code;
     std::string log;
-    if (!jit_compile(src, arch, &code, &log, slp)) {
+    if (!jit_compile(src, arch, &code, &log)) {
       e->why = "hipRTC compile failed: " + log.substr(0, 2000);
     } else if (hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
                hipModuleGetFunction(&e->k.render, e->mod, (prefix + "_render").c_str()) != hipSuccess ||
@@ -175,7 +174,7 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
   }
   out->visits = visits;
   out->folded = folded;
-  return build_module(src, "rt_static", out, why, (variant & kVarNoise) == 0);
+  return build_module(src, "rt_static", out, why);
 }
 
 int scene_shading_bits(const SceneImage &img) {

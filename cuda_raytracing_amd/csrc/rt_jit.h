@@ -27,8 +27,7 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
                 bool *folded = nullptr);
 // Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
-bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log,
-                 bool slp = false);
+bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
 
 // Per-lane DFS kernels specialised on the node kinds present in the scene (large scenes: the
 // kind dispatch of trav_step keeps only those branches).  Same contract as jit_kernels.
