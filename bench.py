@@ -290,7 +290,7 @@ def main():
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": load_traffic(workload),
                 "ops_per_sample": round(ops_per_sample, 1),
-                "measured_on": "isolated frame: render-kernel HIP events on its stream",
+                "measured_on": "median of three isolated frames: render-kernel HIP events on its stream",
                 "counters_per_sample": {k: round(v / max(counters["samples"], 1), 4) for k, v in counters.items()
                                         if k not in ("samples", "max_stack", "stack_overflow", "rng_draws")},
             },
