@@ -193,8 +193,9 @@ def main():
 
     def launch(k):
         i = k % nf
-        ctxs[i].render_into(cam, params, outs[i].data_ptr(), streams[i].cuda_stream)
-        rt.tonemap_device(outs[i], outs8[i], streams[i].cuda_stream)   # PPM bytes on the device
+        # the render kernel writes each finished pixel's PPM bytes too (no separate tonemap pass
+        # queued behind the next frame's render blocks)
+        ctxs[i].render_into(cam, params, outs[i].data_ptr(), streams[i].cuda_stream, outs8[i].data_ptr())
         pending.append(i)
 
     def retire():
@@ -270,7 +271,7 @@ def main():
                 "workload": workload,
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "parallelism": f"rows interleaved x{world_size}" + ((" + RCCL u8 gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} u8 gather") if world_size > 1 else ""),
-                "output": "PPM bytes on the device (rt_tonemap_device)",
+                "output": "PPM bytes written by the render kernel (rt_context_render_ppm)",
                 "pixels_per_gpu": rows * W,
                 "frames_in_flight": nf,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),

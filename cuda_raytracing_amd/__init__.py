@@ -248,7 +248,15 @@ class RenderContext:
         self._h = h
         self._scene = scene
 
-    def render_into(self, camera: Camera, params: Params, out_device_ptr: int, stream: int = 0) -> None:
+    def render_into(self, camera: Camera, params: Params, out_device_ptr: int, stream: int = 0,
+                    out_ppm_device_ptr: int = 0) -> None:
+        """Render into a device float buffer; with out_ppm_device_ptr also the P6 payload bytes, written
+        by the render kernel as it finishes each pixel (rt_context_render_ppm)."""
+        if out_ppm_device_ptr:
+            _check(self._L.rt_context_render_ppm(self._h, C.byref(camera), C.byref(params), C.c_void_p(out_device_ptr),
+                                                 C.c_void_p(out_ppm_device_ptr), C.c_void_p(stream)),
+                   "rt_context_render_ppm")
+            return
         _check(self._L.rt_context_render(self._h, C.byref(camera), C.byref(params),
                                          C.c_void_p(out_device_ptr), C.c_void_p(stream)), "rt_context_render")
 

@@ -164,7 +164,7 @@ def host_lib():
     return _host
 
 
-HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_timing",
+HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_render_ppm", "rt_context_timing",
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
                "rt_seed_states"]
@@ -198,6 +198,7 @@ def hip_lib():
              C.POINTER(Stats))
         _sig(L.rt_context_create, C.c_int, C.POINTER(Scene), C.c_int, C.POINTER(C.c_void_p))
         _sig(L.rt_context_render, C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P)
+        _sig(L.rt_context_render_ppm, C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P, P)
         _sig(L.rt_context_timing, C.c_int, P, C.POINTER(Stats))
         _sig(L.rt_context_destroy, None, P)
         _sig(L.rt_status_string, C.c_char_p, C.c_int)

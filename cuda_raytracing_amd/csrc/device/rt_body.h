@@ -903,6 +903,14 @@ struct PacketTrace {
   }
 };
 
+// linear -> P6 byte of pixels_to_ppm (raytracing.cu:1391-1395, 1419-1431): sqrt gamma (0 for
+// non-positive), clamp to [0, 0.999], (u8)(256 x) — the conversion of rt_tonemap / tonemap_kernel
+__device__ __forceinline__ uint8_t ppm_byte(float c) {
+  const float g = c > 0 ? sqrtf(c) : 0.0f;
+  const float k = (g < 0.0f) ? 0.0f : ((g > 0.999f) ? 0.999f : g);
+  return static_cast<uint8_t>(static_cast<uint32_t>(256 * k) & 0xffu);
+}
+
 // ---------------------------------------------------------------------------------------------
 // the render body (cuda_calc + ray_color)
 // ---------------------------------------------------------------------------------------------
@@ -1278,9 +1286,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         busy = false;
       } else if (sample == A.spp) {
         float *o = A.out + 3 * static_cast<size_t>(pix);
-        o[0] = sum.x * A.sample_scale;
-        o[1] = sum.y * A.sample_scale;
-        o[2] = sum.z * A.sample_scale;
+        const f3 c = mk(sum.x * A.sample_scale, sum.y * A.sample_scale, sum.z * A.sample_scale);
+        o[0] = c.x;
+        o[1] = c.y;
+        o[2] = c.z;
+        if (A.out8) {   // pixels_to_ppm's bytes of the same floats (:1391-1395, 1419-1431), fused
+          uint8_t *b = A.out8 + 3 * static_cast<size_t>(pix);
+          b[0] = ppm_byte(c.x);
+          b[1] = ppm_byte(c.y);
+          b[2] = ppm_byte(c.z);
+        }
         busy = false;
       } else {
         camera_ray();

@@ -115,6 +115,7 @@ struct RenderArgs {
   uint32_t n_ids;             // 64 * ceil(rows/8) * tiles_x: tile-major pixel ids handed to waves
   const uint32_t *rng;        // [6][n_pixels] seeded XORWOW states {d, x0..x4}
   float *out;                 // [n_pixels][3]
+  uint8_t *out8;              // optional [n_pixels][3] P6 payload bytes (pixels_to_ppm), null = none
   float *rc;                  // attenuation stack: [max_bounces][3][threads]
   uint32_t threads;           // grid size in threads (rc stride)
   uint32_t *work;             // chunk counter (zeroed per launch)

@@ -304,6 +304,11 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
 }
 
 int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, float *out_dev, void *stream) {
+  return rt_context_render_ppm(c, cam, p, out_dev, nullptr, stream);
+}
+
+int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *p, float *out_dev, uint8_t *out8_dev,
+                          void *stream) {
   if (!c || !cam) return RT_ERR_INVALID_ARG;
   int st = params_check(p);
   if (st != RT_OK) return st;
@@ -324,6 +329,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     (void)hipEventRecord(c->ev[1], s);
     (void)hipEventRecord(c->ev[3], s);
     if (hipMemsetAsync(out_dev, 0, static_cast<size_t>(n) * 12, s) != hipSuccess) return RT_ERR_HIP;
+    if (out8_dev && hipMemsetAsync(out8_dev, 0, static_cast<size_t>(n) * 3, s) != hipSuccess) return RT_ERR_HIP;
     (void)hipEventRecord(c->ev[2], s);
     return RT_OK;
   }
@@ -479,6 +485,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
   a.n_ids = 64u * ((a.rows + 7) / 8) * a.tiles_x;
   a.rng = static_cast<const uint32_t *>(c->rng.p);
   a.out = out_dev;
+  a.out8 = out8_dev;
   a.rc = static_cast<float *>(c->rc.p);
   a.threads = threads;
   a.work = static_cast<uint32_t *>(c->work.p);
@@ -522,6 +529,7 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
     pa.n_ids = n_tiles * pa.probe_per_tile;
     pa.spp = 1;
     pa.out = nullptr;
+    pa.out8 = nullptr;
     pa.rng = nullptr;
     pa.work = static_cast<uint32_t *>(c->work.p) + 8;
     pa.wave_trace = nullptr;

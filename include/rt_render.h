@@ -138,6 +138,11 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out);
  * stream).  Asynchronous; timings are read with rt_context_timing() after the stream completes. */
 int rt_context_render(rt_context *ctx, const rt_camera *camera, const rt_params *params,
                       float *out_rgb_device, void *stream);
+/* rt_context_render that also writes the P6 payload (3 bytes per pixel, pixels_to_ppm's conversion,
+ * raytracing.cu:1391-1395,1419-1431, bit-identical to rt_tonemap) of every pixel as the render kernel
+ * finishes it, into out_ppm_device (row_count*width*3 bytes): no separate tonemap pass. */
+int rt_context_render_ppm(rt_context *ctx, const rt_camera *camera, const rt_params *params,
+                          float *out_rgb_device, uint8_t *out_ppm_device, void *stream);
 /* Blocks on the last render's events; fills init/render ms, samples and (if counted) counters. */
 int rt_context_timing(rt_context *ctx, rt_stats *stats);
 void rt_context_destroy(rt_context *ctx);

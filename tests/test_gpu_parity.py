@@ -401,3 +401,22 @@ def test_cli_writes_the_oracle_ppm(scene, args, tmp_path):
     header = f"P6\n{W} {H}\n255\n".encode()
     assert data.startswith(header)
     assert data[len(header):] == rt.tonemap(ref).tobytes()
+
+
+@pytest.mark.parametrize("idx,W,H,spp,b", [(0, 96, 54, 8, 16), (17, 64, 36, 4, 50), (1, 40, 40, 4, 50), (0, 33, 7, 2, 0)])
+def test_fused_ppm_bytes_match_host_tonemap(idx, W, H, spp, b):
+    # rt_context_render_ppm: the render kernel writes each finished pixel's P6 bytes; they must equal the
+    # host pixels_to_ppm conversion of the float frame it writes alongside (b = 0: the all-zero path)
+    import torch
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=b)
+    ctx = rt.RenderContext(w.scene(), 0)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    out8 = torch.full((H, W, 3), 7, dtype=torch.uint8, device="cuda")
+    ctx.render_into(cam, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream, out8.data_ptr())
+    torch.cuda.synchronize()
+    fb = out.cpu().numpy()
+    assert np.array_equal(out8.cpu().numpy(), rt.tonemap(fb))
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
