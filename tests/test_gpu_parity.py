@@ -491,3 +491,45 @@ def test_random_scenes_vs_oracle(seed):
         p.flags = force
         fb, _ = gpu(w.scene(), cam, p)
         assert np.array_equal(bits(fb), bits(ref)), force
+
+
+def _random_sphere_world(seed: int):
+    """All-sphere world for the verified SAH walk: random sizes (incl. a ground sphere), exact
+    duplicates (bitwise-equal roots: the tie fallback), moving spheres, every material kind."""
+    g = np.random.default_rng(1000 + seed)
+    w = rt.World(capacity=2048)
+    mats = [w.lambert((0.5, 0.5, 0.5)), w.metal((0.8, 0.7, 0.6), 0.2), w.dielectric(1.5),
+            w.light((4.0, 4.0, 4.0)), w.checker(1.0, (0.2, 0.3, 0.1), (0.9, 0.9, 0.9))]
+    w.sphere((0.0, -1000.0, 0.0), 1000.0, mats[0])
+    n = int(g.integers(64, 400))
+    for k in range(n):
+        c = (float(g.uniform(-8, 8)), float(g.uniform(0, 3)), float(g.uniform(-8, 8)))
+        r = float(g.choice([0.05, 0.2, 0.5, 1.0, float(g.uniform(0.01, 2))]))
+        m = mats[int(g.integers(0, len(mats)))]
+        if k % 17 == 0:
+            w.moving_sphere(c, (0.0, float(g.uniform(0, 0.5)), 0.0), r, m)
+        else:
+            w.sphere(c, r, m)
+        if k % 23 == 0:
+            w.sphere(c, r, m)   # exact duplicate: equal roots, the reference's DFS order decides
+    s = rt.Settings()
+    _abi.host_lib().rt_settings_default(C.byref(s))
+    s.lookfrom = rt.vec3(float(g.uniform(-12, 12)), float(g.uniform(1, 6)), float(g.uniform(-12, 12)))
+    s.lookat = rt.vec3(0.0, 0.5, 0.0)
+    s.vfov = float(g.uniform(20, 70))
+    s.defocus_angle = float(g.choice([0.0, 0.6]))
+    s.background = rt.vec3(0.7, 0.8, 1.0)
+    return w, s
+
+
+@pytest.mark.parametrize("seed", list(range(int(__import__("os").environ.get("RT_FUZZ_SEEDS", "12")) // 2)))
+def test_random_sphere_worlds_verified_walk(seed):
+    w, s = _random_sphere_world(seed)
+    cam, W, H = rt.camera_from_settings(s, 64, 36)
+    p = rt.make_params(s, W, H, spp=4, bounces=12)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    p.flags = rt.RT_FLAG_FORCE_ACCEL
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_ACCEL
+    assert np.array_equal(bits(fb), bits(ref))
