@@ -966,7 +966,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool exhausted = false;
   uint32_t tiles_taken = 0, rounds = 0;
   uint32_t probe_tile = 0, probe_rounds = 0;
-  uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, t_mark = 0;   // wave-trace clocks
+  uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, ph_unwind = 0, ph_cam = 0, t_mark = 0;   // wave-trace clocks
   uint64_t busy_lane_rounds = 0;
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
 
@@ -1278,6 +1278,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
         }
       }
+      if (TRACE) {   // the unwind's share of the done block (the rest: camera ray / pixel write)
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        ph_unwind += t - t_mark;
+        t_mark = t;
+      }
       sum = add(sum, res);
       sample++;
       if (COUNT) c_samples++;
@@ -1300,6 +1305,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       } else {
         camera_ray();
       }
+      if (TRACE) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        ph_cam += t - t_mark;
+        t_mark = t;
+      }
     }
   }
 
@@ -1310,7 +1320,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     unsigned long long *w = A.wave_trace + kWaveTraceWords * static_cast<size_t>(blockIdx.x * kWavesPerBlock + wave);
     w[0] = t_start; w[1] = t_end; w[2] = tiles_taken; w[3] = (static_cast<uint64_t>(xcc) << 32) | hw;
     w[4] = rounds; w[5] = busy_lane_rounds;
-    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade; w[9] = ph_mat; w[10] = ph_rej;
+    w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade; w[9] = ph_mat; w[10] = ph_rej; w[11] = ph_unwind;
+    w[12] = ph_cam;
   }
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};

@@ -84,7 +84,7 @@ constexpr int kDeepBounces = 16;
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
-constexpr uint32_t kWaveTraceWords = 11;
+constexpr uint32_t kWaveTraceWords = 13;
 
 // Resident 256-thread blocks per CU allowed by the VGPR budget: 512 VGPRs per lane per SIMD, one
 // wave of each block per SIMD.  The persistent grid must never exceed residency (a block that starts

@@ -27,7 +27,7 @@ import cuda_raytracing_amd as rt  # noqa: E402
 w, s = rt.build_scene(a.scene)
 cam, W, H = rt.camera_from_settings(s, a.width, a.height)
 fb, st = rt.render(w.scene(), cam, rt.make_params(s, W, H, spp=a.spp, bounces=a.bounces), with_stats=True)
-rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 11)
+rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 13)
 rec = rec[rec[:, 1] > 0]
 t0 = rec[:, 0].min()
 start = (rec[:, 0] - t0).astype(np.float64)
@@ -42,9 +42,9 @@ tiles = rec[:, 2].astype(np.int64)
 print("tiles/wave: min %d mean %.2f max %d" % (tiles.min(), tiles.mean(), tiles.max()))
 rounds = rec[:, 4].astype(np.float64); busy = rec[:, 5].astype(np.float64)
 print("busy lanes per round (wave mean): %.1f of 64; rounds/wave mean %.0f" % (busy.sum() / rounds.sum(), rounds.mean()))
-ph = rec[:, 6:11].astype(np.float64).sum(axis=0)
-print("phase cycles: refill %.1f%%  traverse %.1f%%  unwind+camera %.1f%%  material+scatter %.1f%%  rejection %.1f%%"
-      % tuple(100 * ph / ph.sum()))
+ph = rec[:, 6:13].astype(np.float64).sum(axis=0)
+print("phase cycles: refill %.1f%%  traverse %.1f%%  loop-back %.1f%%  material+scatter %.1f%%  rejection %.1f%%  unwind %.1f%%  "
+      "sum+camera/write %.1f%%" % tuple(100 * ph / ph.sum()))
 xcc = (rec[:, 3] >> np.uint64(32)).astype(np.int64)
 for x in np.unique(xcc):
     m = xcc == x
@@ -52,11 +52,11 @@ for x in np.unique(xcc):
 top = np.argsort(-end)[:5]
 for w in top:
     r = rec[w]
-    ph = r[6:11].astype(np.float64)
+    ph = r[6:13].astype(np.float64)
     print(f"straggler wave {w}: end {100 * end[w] / span:.1f}% rounds {int(r[4])} busy-lane-rounds {int(r[5])} "
           f"tiles {int(r[2])} us/round {(end[w] - start[w]) / 100 / max(int(r[4]), 1):.2f} phases (cycles/round): "
           + " ".join(f"{n} {v / max(int(r[4]), 1):.0f}" for n, v in
-                     zip(("refill", "trace", "unwind+cam", "mat", "rej"), ph)))
+                     zip(("refill", "trace", "back", "mat", "rej", "unwind", "cam"), ph)))
 # per dispatch rank: block b reaches its CU in round b // n_cu of the dispatch (n_cu = 256 blocks
 # per round on MI355X), so its waves are the (b // n_cu)-th oldest of their SIMDs
 wid = np.arange(len(rec))
