@@ -2,23 +2,26 @@
 """bench.py — Msamples/s of the per-pixel render path on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scene 0] [--width 1920] [--height 1080]
-                    [--spp 512] [--bounces 16] [--inflight 2] [--no-cpu-baseline]
+                    [--spp 512] [--bounces 16] [--frame weak|fixed] [--pipelined-steps K2]
+                    [--no-cpu-baseline] [--no-e2e]
 
-A "step" is one frame: RNG seeding + longest-first schedule probe + render kernel + device tonemap
-to PPM bytes (+ the RCCL gather of the u8 rows to rank 0 when N>1), with the scene already resident
-in HBM.  Default workload = BASELINE
-config 2: scene 0 (fv1) at 1920x1080, spp 512, depth 16 on one GPU.  With N ranks
-(torch.distributed.run, one process per GPU, backend "nccl" = RCCL) the frame grows to ~N x the
-pixels at the same aspect and camera (weak scaling) and rows are interleaved across ranks.  Up to
---inflight frames are queued at once on separate streams (frames are independent; the next frame
-fills the SIMDs the previous frame's slowest pixels leave idle).  Rank 0 prints ONE JSON line.
-
-The printed value is samples of all ranks x K frames / max-over-ranks wall time of the K timed steps.
-roofline: VALU-bound kernel; achieved = algorithmic FP32 ops per render launch (op model of
-SURVEY §8d evaluated on this workload's measured per-sample visit counts) / the render kernel's
-HIP-event duration on an isolated frame (no overlap; profile with --inflight 1 to compare with
-rocprofv3).  cpu_baseline: the C oracle on this host's cores over a bounded row sample, whose GPU
-render is compared bit for bit.
+A "step" is one frame, rendered to completion before the next starts — the reference's metric is one
+cuda_calc launch (raytracing.cu:1752-1768): RNG seeding + longest-first schedule probe + render kernel
+writing float RGB and PPM bytes (+ the RCCL gather of the u8 rows to rank 0 when N>1), with the scene
+already resident in HBM.  Default workload = BASELINE config 2: scene 0 (fv1) at 1920x1080, spp 512,
+depth 16 on one GPU.  With N ranks (torch.distributed.run, one process per GPU, backend "nccl" = RCCL)
+rows are interleaved across ranks and
+  --frame weak  (default) the frame grows to ~N x the pixels at the same aspect and camera;
+  --frame fixed the stated W x H is split N ways (BASELINE configs 4 and 5: one frame over 8 GPUs).
+Rank 0 prints ONE JSON line.  value = samples of all ranks x K / max-over-ranks wall time of the K
+timed frames.  Secondary keys: `pipelined` (2 frames in flight on two streams: the next frame fills
+the SIMDs the previous frame's last pixels leave idle), `e2e` (bin/raytracing wall time of the whole
+reference render() region, cold and warm code-object cache), `cpu_baseline` (the C oracle built
+-O3 -march=native on this host, all cores and 1 core, on a bounded row sample whose GPU render is
+compared bit for bit).
+roofline: VALU-bound kernel; achieved = algorithmic FP32 ops per render launch (op model of SURVEY §8d
+on this workload's measured per-sample visit counts) / the render kernel's median HIP-event duration
+over the timed frames (events on the launch stream; rocprofv3 sees the same launches).
 """
 from __future__ import annotations
 
@@ -26,7 +29,10 @@ import argparse
 import json
 import math
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -63,19 +69,50 @@ def op_model(counters: dict, samples: int) -> float:
     return ops / max(samples, 1)
 
 
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def baseline_oracle():
+    """The oracle built for speed on THIS host (BASELINE.md CPU plan: -O3 -march=native -fopenmp), from
+    the same source and with the same parity flags (no FP contraction, IEEE div/sqrt).  Built into a
+    temporary directory at run time because -march=native must describe the box's own CPU; falls back
+    to the prebuilt -O2 test build if no compiler is usable."""
+    src = REPO / "oracle" / "oracle_rt.c"
+    flags = ["-O3", "-march=native", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fopenmp"]
+    d = Path(tempfile.mkdtemp(prefix="rt_cpu_baseline_"))
+    lib = d / "liboracle_rt_native.so"
+    try:
+        r = subprocess.run([os.environ.get("CC", "cc"), *flags, "-I", str(REPO / "include"), "-shared", str(src),
+                            "-o", str(lib), "-lm"], capture_output=True, text=True, timeout=120)
+        if r.returncode == 0 and lib.exists():
+            return _abi.oracle_lib(lib), " ".join(flags)
+        log(f"cpu baseline: native build failed ({r.stderr.strip()[:200]}); using the -O2 test build")
+    except (OSError, subprocess.TimeoutExpired) as e:
+        log(f"cpu baseline: native build failed ({e}); using the -O2 test build")
+    return _abi.oracle_lib(), "-O2 -std=c11 -ffp-contract=off -fno-fast-math -fopenmp (prebuilt test build)"
+
+
 def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
-    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample.
+    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample, all cores and 1 core.
 
     The same sample is then rendered on the GPU through the product context and compared bit for bit
     (the PSNR half of the BASELINE metric: identical frames -> PSNR = inf, reported as "bit-exact")."""
     import ctypes as C
     import numpy as np
-    L = _abi.oracle_lib()
+    L, build = baseline_oracle()
+    threads = int(L.rt_oracle_threads())
     cam, W, H = rt.camera_from_settings(settings, W, H)
 
-    def run(stride, s):
-        rows = len(range(0, H, stride))
-        p = rt.make_params(settings, W, H, spp=s, bounces=bounces, row_offset=0, row_stride=stride, row_count=rows)
+    def run(stride, s, offset=0):
+        rows = len(range(offset, H, stride))
+        p = rt.make_params(settings, W, H, spp=s, bounces=bounces, row_offset=offset, row_stride=stride, row_count=rows)
         out = np.zeros((rows, W, 3), np.float32)
         st = _abi.Stats()
         t = time.perf_counter()
@@ -85,25 +122,33 @@ def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
         assert rc == 0, rc
         return rows * W * s, dt, out
 
-    # calibrate on a sparse row sample (twice: the first call also spins up the OpenMP pool), then
-    # render every stride-th row of the frame at the FULL spp so the per-pixel work equals the GPU's
-    # calibrate: t = a*pixels (RNG seeding by jumps) + b*samples, from two short runs on every 16th row
+    def sample_stride(budget):
+        # calibrate: t = a*pixels (RNG seeding by jumps) + b*samples, from two short runs on every 16th row
+        # (run twice at first: the first call also spins up the OpenMP pool)
+        s1, s2 = min(spp, 8), min(spp, 32)
+        n1, t1, _ = run(16, s1)
+        n2, t2, _ = run(16, s2)
+        px = n1 / s1
+        b = max((t2 - t1) / max(n2 - n1, 1), 1e-12) if s2 > s1 else t1 / n1
+        a = max((t1 - b * n1) / px, 0.0)
+        return max(1, math.ceil((a * W * H + b * W * H * spp) / budget))
+
+    # all cores: every stride-th row of the frame at the FULL spp, so the per-pixel work equals the GPU's
     run(16, 2)
-    s1, s2 = min(spp, 8), min(spp, 32)
-    n1, t1, _ = run(16, s1)
-    n2, t2, _ = run(16, s2)
-    px = n1 / s1
-    b = max((t2 - t1) / max(n2 - n1, 1), 1e-12) if s2 > s1 else t1 / n1
-    a = max((t1 - b * n1) / px, 0.0)
-    full_s = a * W * H + b * W * H * spp
-    stride = max(1, math.ceil(full_s / budget_s))
-    rows = len(range(0, H, stride))
-    s = spp
-    n, dt, ref = run(stride, s)
+    stride = sample_stride(budget_s)
+    n, dt, ref = run(stride, spp)
+    rows = ref.shape[0]
+    # one core: a quarter of the budget on a sparser row set (same per-sample work)
+    L.rt_oracle_set_threads(1)
+    try:
+        stride1 = sample_stride(budget_s / 4)
+        n1, dt1, _ = run(stride1, spp, offset=stride1 // 2)
+    finally:
+        L.rt_oracle_set_threads(threads)
     parity = None
     if ctx is not None:
         import torch
-        p = rt.make_params(settings, W, H, spp=s, bounces=bounces, row_offset=0, row_stride=stride, row_count=rows)
+        p = rt.make_params(settings, W, H, spp=spp, bounces=bounces, row_offset=0, row_stride=stride, row_count=rows)
         dev = torch.empty((rows, W, 3), dtype=torch.float32, device="cuda")
         ctx.render_into(cam, p, dev.data_ptr(), torch.cuda.current_stream().cuda_stream)
         ctx.timing()
@@ -112,11 +157,53 @@ def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
         parity = {"bit_exact": bool(np.array_equal(g.view(np.uint32), ref.view(np.uint32))),
                   "psnr_db": None if mse == 0 else round(10 * math.log10(1.0 / mse), 2),
                   "note": "GPU vs oracle on this sample; psnr_db null = identical frames (PSNR infinite)"}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {
-        "value": n / dt / 1e6, "unit": "Msamples/s", "cores": int(L.rt_oracle_threads()), "kind": "port",
-        "sample": f"frame rows 0::{stride} ({rows} rows x {W} px) at spp {s}, d{bounces}: {n:.3g} samples in {dt:.1f} s",
+        "value": round(n / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
+        "sample": f"frame rows 0::{stride} ({rows} rows x {W} px) at spp {spp}, d{bounces}: {n:.3g} samples in {dt:.1f} s",
+        "single_core": {"value": round(n1 / dt1 / 1e6, 3), "unit": "Msamples/s", "cores": 1,
+                        "sample": f"frame rows {stride1 // 2}::{stride1} at spp {spp}: {n1:.3g} samples in {dt1:.1f} s"},
+        "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity,
+        "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "build": build,
         "parity": parity,
     }
+
+
+def e2e_cli(scene: int, W: int, H: int, spp: int, bounces: int):
+    """End-to-end wall time of `bin/raytracing` (the reference's `./raytracing scene sN bN` plus the
+    resolution flags): scene build, BVH, kernel compile or code-object cache load, upload, RNG seeding,
+    render, D2H copy and PPM write (raytracing.cu:1649-1773).  Cold = empty code-object cache (hipRTC
+    compiles), warm = a second process that loads the cached code object."""
+    exe = REPO / "bin" / "raytracing"
+    if not exe.exists():
+        return {"error": "bin/raytracing not built"}
+    d = Path(tempfile.mkdtemp(prefix="rt_e2e_"))
+    env = dict(os.environ, RT_JIT_CACHE_DIR=str(d / "cache"))
+    res = {"command": f"bin/raytracing {scene} s{spp} b{bounces} w{W} h{H}"}
+    try:
+        for leg in ("cold", "warm"):
+            t = time.perf_counter()
+            r = subprocess.run([str(exe), str(scene), f"s{spp}", f"b{bounces}", f"w{W}", f"h{H}"], cwd=d,
+                               capture_output=True, text=True, timeout=600, env=env)
+            wall = time.perf_counter() - t
+            if r.returncode != 0:
+                return {"error": (r.stdout + r.stderr)[-400:]}
+            info = {"process_wall_ms": round(wall * 1e3, 1)}
+            for line in r.stdout.splitlines():
+                if line.startswith("End-to-end:"):
+                    info["e2e_ms"] = round(float(line.split(":")[1].split("ms")[0]), 1)
+                    info["kernels"] = line.split("[", 1)[1].split("]", 1)[0]
+                elif line.startswith("Rendering time:") and line.rstrip().endswith("ms"):
+                    info["render_ms"] = round(float(line.split(":")[1].split("ms")[0]), 3)
+                elif line.startswith("RNG seeding time:"):
+                    info["seed_ms"] = round(float(line.split(":")[1].split("ms")[0]), 3)
+            res[leg] = info
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return res
 
 
 def load_traffic(workload: str):
@@ -140,9 +227,13 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=512)
     ap.add_argument("--bounces", type=int, default=16)
+    ap.add_argument("--frame", choices=("weak", "fixed"), default="weak",
+                    help="N>1: weak = ~N x the pixels (fixed work per GPU), fixed = the stated frame split N ways")
+    ap.add_argument("--pipelined-steps", type=int, default=-1,
+                    help="frames of the secondary 2-in-flight measurement (default: --steps; 0 = skip)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of oracle wall time (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2, help="frames queued at once (own context + stream each)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the bin/raytracing end-to-end leg")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (plumbing rehearsal)")
     args = ap.parse_args()
 
@@ -161,47 +252,45 @@ def main():
 
     # ---- host pre-pass (untimed, like the reference's make_bvh + camera) ----
     world, settings = rt.build_scene(args.scene)
-    W, H = weak_scaled_resolution(args.width, args.height, world_size)
+    if args.frame == "weak":
+        W, H = weak_scaled_resolution(args.width, args.height, world_size)
+    else:
+        W, H = args.width, args.height
     cam, W, H = rt.camera_from_settings(settings, W, H)
     off, stride, rows = rt.shard_rows(H, rank, world_size)
     params = rt.make_params(settings, W, H, spp=args.spp, bounces=args.bounces,
                             row_offset=off, row_stride=stride, row_count=rows)
-    nf = max(1, args.inflight)
-    ctxs = [rt.RenderContext(world.scene(), device=dev) for _ in range(nf)]
+    ctxs = [rt.RenderContext(world.scene(), device=dev) for _ in range(2)]
     ctx = ctxs[0]
-    streams = [torch.cuda.Stream() for _ in range(nf)]
-    outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(nf)]
-    outs8 = [torch.empty((rows, W, 3), dtype=torch.uint8, device="cuda") for _ in range(nf)]
-    stream, out = streams[0], outs[0]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    outs = [torch.empty((rows, W, 3), dtype=torch.float32, device="cuda") for _ in range(2)]
+    outs8 = [torch.empty((rows, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     workload = f"scene{args.scene}_{rt.scene_name(args.scene)}_{W}x{H}_spp{args.spp}_d{args.bounces}"
 
     # ---- op model: per-sample event rates of THIS workload (counting variant, untimed) ----
     model_spp = min(args.spp, 8)
     pc = rt.make_params(settings, W, H, spp=model_spp, bounces=args.bounces,
                         row_offset=off, row_stride=stride, row_count=rows, flags=rt.RT_FLAG_COUNT)
-    ctx.render_into(cam, pc, out.data_ptr(), stream.cuda_stream)
+    ctx.render_into(cam, pc, outs[0].data_ptr(), streams[0].cuda_stream)
     cst = ctx.timing()
     counters = cst.counter_dict()
     ops_per_sample = op_model(counters, counters["samples"])
 
-    # Frames are independent, so up to `inflight` frames are queued on their own streams (each with its
-    # own context: RNG states, colour stack, schedule): the next frame's blocks fill the SIMDs that
-    # the previous frame's last pixels leave idle, and the rank-0 gather of frame k overlaps frame k+1.
-    # Every frame is rendered completely; the timed region ends when the last one is retired.
     pending = []
     stats = []
 
-    def launch(k):
+    def launch(k, nf):
         i = k % nf
-        # the render kernel writes each finished pixel's PPM bytes too (no separate tonemap pass
-        # queued behind the next frame's render blocks)
+        # the slot's buffers may still be read by the previous frame's gather on the current stream
+        streams[i].wait_stream(torch.cuda.current_stream())
+        # the render kernel writes each finished pixel's PPM bytes too (no separate tonemap pass)
         ctxs[i].render_into(cam, params, outs[i].data_ptr(), streams[i].cuda_stream, outs8[i].data_ptr())
         pending.append(i)
 
     def retire():
         i = pending.pop(0)
         st = ctxs[i].timing()                                  # waits on that frame's render events
-        torch.cuda.current_stream().wait_stream(streams[i])    # ... and its tonemap
+        torch.cuda.current_stream().wait_stream(streams[i])
         if world_size > 1:
             if args.dist_backend == "nccl":
                 gather_rows(outs8[i], H, W, rank, world_size)  # u8 rows: 3 B/pixel over xGMI
@@ -209,52 +298,59 @@ def main():
                 gather_rows(outs8[i].cpu(), H, W, rank, world_size)
         stats.append(st)
 
-    def run(frames):
+    def run(frames, nf):
         for k in range(frames):
             if len(pending) == nf:
                 retire()
-            launch(k)
+            launch(k, nf)
         while pending:
             retire()
 
-    run(max(args.warmup, 1) if nf > 1 else args.warmup)
-    # isolated frames: the render kernel's own duration for the roofline (no overlap); the median
-    # of three, since one frame's tail varies by a few percent from run to run
-    isos = []
-    for _ in range(3):
-        launch(0)
-        retire()
-        isos.append(stats[-1])
-    iso = sorted(isos, key=lambda st: st.render_ms)[1]
-    stats.clear()
-    if world_size > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    if world_size > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world_size > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        if args.dist_backend != "nccl":
-            t = t.cpu()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    render_ms = [st.render_ms for st in stats]
-    init_ms = [st.init_ms for st in stats]
-    sched_ms = [st.sched_ms for st in stats]
+    def timed(frames, nf):
+        stats.clear()
+        if world_size > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(frames, nf)
+        if world_size > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world_size > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            if args.dist_backend != "nccl":
+                t = t.cpu()
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, list(stats)
 
     samples_per_step = W * H * args.spp                  # all ranks together
-    value = samples_per_step * args.steps / elapsed / 1e6
-    mean_render_ms = iso.render_ms
     local_samples = rows * W * args.spp
-    achieved = ops_per_sample * local_samples / (mean_render_ms / 1e3) / 1e12
+
+    # ---- headline: one frame at a time (the reference's one-launch metric) ----
+    run(args.warmup, 1)
+    elapsed, fstats = timed(args.steps, 1)
+    value = samples_per_step * args.steps / elapsed / 1e6
+    med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+    render_ms = med([st.render_ms for st in fstats])
+    seed_ms = med([st.init_ms for st in fstats])
+    sched_ms = med([st.sched_ms for st in fstats])
+    achieved = ops_per_sample * local_samples / (render_ms / 1e3) / 1e12
+
+    # ---- secondary: two frames in flight (independent frames overlap their tails) ----
+    psteps = args.steps if args.pipelined_steps < 0 else args.pipelined_steps
+    pipelined = None
+    if psteps > 0:
+        run(2, 2)
+        pel, pst = timed(psteps, 2)
+        pipelined = {"value": round(samples_per_step * psteps / pel / 1e6, 2), "unit": "Msamples/s",
+                     "frames_in_flight": 2, "steps": psteps, "ms_per_step": round(pel / psteps * 1e3, 3),
+                     "render_ms_mean": round(sum(st.render_ms for st in pst) / len(pst), 3)}
 
     if rank == 0:
         line = {
-            "metric": f"Msamples/sec (pixels x spp / s) at {args.width}x{args.height} spp={args.spp} d={args.bounces}"
+            "metric": f"Msamples/sec (pixels x spp / s) at {W}x{H} spp={args.spp} d={args.bounces}"
                       + (f" scene {args.scene}" if args.scene != 0 else ""),
             "value": round(value, 2),
             "unit": "Msamples/s",
@@ -263,26 +359,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if (args.frame == "weak" or world_size == 1) else "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic: reference scene catalog rebuilt on the host (glibc-rand seed 1), XORWOW seed 1234",
             "config": {
                 "workload": workload,
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
+                "frame": args.frame,
                 "parallelism": f"rows interleaved x{world_size}" + ((" + RCCL u8 gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} u8 gather") if world_size > 1 else ""),
-                "output": "PPM bytes written by the render kernel (rt_context_render_ppm)",
+                "step": "one frame to completion: RNG seed + schedule probe + render (float RGB + PPM bytes)"
+                        + (" + gather to rank 0" if world_size > 1 else ""),
                 "pixels_per_gpu": rows * W,
-                "frames_in_flight": nf,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
                 "kernel": {rt.RT_TRAV_STATIC: "rt_static_render (hipRTC)", rt.RT_TRAV_ACCEL: "rt_accel_render (hipRTC)"}.get(
                     cst.traversal, "rt_lane_render (hipRTC)"),
             },
-            "kernel_ms": {"render_isolated": round(iso.render_ms, 3), "seed_isolated": round(iso.init_ms, 3),
-                          "schedule_isolated": round(iso.sched_ms, 3),
-                          "single_frame_msamples_s": round(local_samples / ((iso.render_ms + iso.init_ms +
-                                                                             iso.sched_ms) / 1e3) / 1e6, 1),
-                          "render_mean_in_flight": round(sum(render_ms) / len(render_ms), 3)},
+            "kernel_ms": {"render_median": round(render_ms, 3), "seed_median": round(seed_ms, 3),
+                          "schedule_median": round(sched_ms, 3),
+                          "render_only_msamples_s": round(local_samples / (render_ms / 1e3) / 1e6, 1)},
+            "pipelined": pipelined,
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved, 3),
@@ -291,16 +387,22 @@ def main():
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": load_traffic(workload),
                 "ops_per_sample": round(ops_per_sample, 1),
-                "measured_on": "median of three isolated frames: render-kernel HIP events on its stream",
+                "measured_on": "median render-kernel HIP-event duration over the timed frames (launch stream)",
                 "counters_per_sample": {k: round(v / max(counters["samples"], 1), 4) for k, v in counters.items()
                                         if k not in ("samples", "max_stack", "stack_overflow", "rng_draws")},
             },
         }
+        if world_size == 1 and not args.no_e2e:
+            try:
+                line["e2e"] = {"config1": e2e_cli(0, 256, 144, 4, 4),
+                               "this_config": e2e_cli(args.scene, W, H, args.spp, args.bounces)}
+            except Exception as e:  # the secondary legs must never hide the GPU number
+                line["e2e"] = {"error": str(e)}
         if world_size == 1 and not args.no_cpu_baseline:
             try:
                 line["cpu_baseline"] = cpu_baseline(world, settings, W, H, args.spp, args.bounces, args.cpu_budget,
                                                     ctx)
-            except Exception as e:  # the baseline must never hide the GPU number
+            except Exception as e:
                 line["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(line), flush=True)
     for c in ctxs:

@@ -95,7 +95,7 @@ class Stats(C.Structure):
         ("sched_ms", C.c_double),
         ("folded", C.c_int32), ("fold_rerenders", C.c_int32),
         ("accel_spheres", C.c_int32), ("accel_depth", C.c_int32),
-        ("accel_fallbacks", C.c_uint32), ("pad_", C.c_uint32),
+        ("accel_fallbacks", C.c_uint32), ("jit_source", C.c_int32), ("jit_ms", C.c_double),
     ]
 
     def counter_dict(self):
@@ -216,23 +216,35 @@ def hip_lib():
     return _hip
 
 
-def oracle_lib():
-    """CPU oracle — test infrastructure only (tests/, smoke(), bench.py cpu_baseline)."""
+_oracle_builds: dict = {}
+
+
+def oracle_lib(path=None):
+    """CPU oracle — test infrastructure only (tests/, smoke(), bench.py cpu_baseline).
+
+    path: another build of oracle/oracle_rt.c (bench.py's -O3 -march=native CPU-baseline build)."""
     global _oracle
-    if _oracle is None:
-        if not ORACLE_LIB.exists():
-            raise RuntimeError(f"{ORACLE_LIB} missing: run `make oracle`")
-        L = C.CDLL(str(ORACLE_LIB))
-        _sig(L.rt_render_cpu, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
-             C.c_void_p, C.POINTER(Stats))
-        _sig(L.rt_oracle_sinf, C.c_float, C.c_float)
-        _sig(L.rt_oracle_pow5f, C.c_float, C.c_float)
-        _sig(L.rt_oracle_atan2f, C.c_float, C.c_float, C.c_float)
-        _sig(L.rt_oracle_acosf, C.c_float, C.c_float)
-        _sig(L.rt_oracle_uniforms, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int)
-        _sig(L.rt_oracle_threads, C.c_int)
+    if path is None and _oracle is not None:
+        return _oracle
+    lib_path = ORACLE_LIB if path is None else Path(path)
+    if str(lib_path) in _oracle_builds:
+        return _oracle_builds[str(lib_path)]
+    if not lib_path.exists():
+        raise RuntimeError(f"{lib_path} missing: run `make oracle`")
+    L = C.CDLL(str(lib_path))
+    _sig(L.rt_render_cpu, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params),
+         C.c_void_p, C.POINTER(Stats))
+    _sig(L.rt_oracle_sinf, C.c_float, C.c_float)
+    _sig(L.rt_oracle_pow5f, C.c_float, C.c_float)
+    _sig(L.rt_oracle_atan2f, C.c_float, C.c_float, C.c_float)
+    _sig(L.rt_oracle_acosf, C.c_float, C.c_float)
+    _sig(L.rt_oracle_uniforms, C.c_int, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int)
+    _sig(L.rt_oracle_threads, C.c_int)
+    _sig(L.rt_oracle_set_threads, C.c_int, C.c_int)
+    _oracle_builds[str(lib_path)] = L
+    if path is None:
         _oracle = L
-    return _oracle
+    return L
 
 
 def status_string(code: int) -> str:

@@ -7,6 +7,7 @@
 // reference derives H = (int)(W / ratio), raytracing.cu:1659-1660).  The device is HIP's current one
 // (select with HIP_VISIBLE_DEVICES).
 // Writes settings.img_name as binary P6 PPM into the current directory, like render() (:1772).
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -15,6 +16,7 @@
 #include "rt_render.h"
 
 int main(int argc, char **argv) {
+  const auto t_start = std::chrono::steady_clock::now();   // end-to-end: scene build .. PPM written
   int scene = 0;
   if (argc > 1) scene = std::atoi(argv[1]);
   rt_world *w = rt_world_create(scene == RT_SCENE_RANDOM_10K ? 24000 : 8000, 10u << 20);
@@ -69,6 +71,11 @@ int main(int argc, char **argv) {
               static_cast<double>(stats.samples) / (stats.render_ms * 1e3));
   if (rt_write_ppm(s.img_name, fb.data(), static_cast<uint32_t>(W), static_cast<uint32_t>(H)) != RT_OK)
     std::fprintf(stderr, "Couldn't open the file for writing\n");
+  const double e2e = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  static const char *jit_names[] = {"none", "in-process", "disk cache", "compiled"};
+  // the reference's render() region (raytracing.cu:1649-1773) plus the scene build before it
+  std::printf("End-to-end: %fms (scene + BVH + kernels [%s, %.1f ms] + upload + seed + render + D2H + PPM), "
+              "rt_render %fms\n", e2e, jit_names[stats.jit_source & 3], stats.jit_ms, stats.total_ms);
   rt_world_destroy(w);
   return 0;
 }

@@ -175,10 +175,13 @@ struct rt_context {
   rt_camera last_cam{};
   rt_params last_params{};
   float *last_out = nullptr;
+  uint8_t *last_out8 = nullptr;
   void *last_stream = nullptr;
   bool rendered = false;
   uint64_t samples = 0;
   size_t lds_bytes = 0;
+  int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
+  double jit_ms = 0.0;            // ... and the host time spent obtaining them
 };
 
 extern "C" {
@@ -283,7 +286,9 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
       dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
     }
   }
-  if (c->img.stack_need > 512) { delete c; return RT_ERR_STACK; }
+  // per-lane u16 stacks of 4 waves x 64 lanes: 512 B per entry; 256 entries (128 KiB) plus the minimum
+  // colour-stack levels is what one 160 KiB block can hold (checked again per render)
+  if (c->img.stack_need > 256) { delete c; return RT_ERR_STACK; }
   c->black_skip = attenuations_finite(c->img);
   if (const char *e = std::getenv("RT_BLACK_SKIP")) c->black_skip = c->black_skip && e[0] != '0';
   DeviceGuard g(device);
@@ -309,7 +314,9 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
 
 int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *p, float *out_dev, uint8_t *out8_dev,
                           void *stream) {
-  if (!c || !cam) return RT_ERR_INVALID_ARG;
+  if (!c) return RT_ERR_INVALID_ARG;
+  c->rendered = false;   // set again once this frame's whole sequence is enqueued
+  if (!cam) return RT_ERR_INVALID_ARG;
   int st = params_check(p);
   if (st != RT_OK) return st;
   if (!out_dev && p->row_count > 0) return RT_ERR_INVALID_ARG;
@@ -317,31 +324,46 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   hipStream_t s = static_cast<hipStream_t>(stream);
   const uint32_t n = static_cast<uint32_t>(p->row_count) * static_cast<uint32_t>(p->width);
   const uint32_t mb = static_cast<uint8_t>(p->max_bounces);   // rc_stack.max_count is u8 (:220,1596)
+  // a frame counts as rendered only once its whole sequence is enqueued: any failure below leaves
+  // rendered == false, so rt_context_timing never reports an earlier frame's events as this one's
+  c->rendered = false;
+  c->jit_why.clear();
   c->counted = (p->flags & RT_FLAG_COUNT) != 0;
   c->samples = static_cast<uint64_t>(n) * static_cast<uint64_t>(p->samples_per_pixel);
-  c->rendered = true;
+  c->used_fold = false;
   if (n == 0) {
-    for (hipEvent_t e : c->ev) (void)hipEventRecord(e, s);
+    for (hipEvent_t e : c->ev)
+      if (hipEventRecord(e, s) != hipSuccess) return RT_ERR_HIP;
+    c->rendered = true;
     return RT_OK;
   }
   if (mb == 0) {   // ray_color returns {0} without tracing (:1339): every pixel is exactly 0
-    (void)hipEventRecord(c->ev[0], s);
-    (void)hipEventRecord(c->ev[1], s);
-    (void)hipEventRecord(c->ev[3], s);
+    if (hipEventRecord(c->ev[0], s) != hipSuccess || hipEventRecord(c->ev[1], s) != hipSuccess ||
+        hipEventRecord(c->ev[3], s) != hipSuccess)
+      return RT_ERR_HIP;
     if (hipMemsetAsync(out_dev, 0, static_cast<size_t>(n) * 12, s) != hipSuccess) return RT_ERR_HIP;
     if (out8_dev && hipMemsetAsync(out8_dev, 0, static_cast<size_t>(n) * 3, s) != hipSuccess) return RT_ERR_HIP;
-    (void)hipEventRecord(c->ev[2], s);
+    if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
+    c->rendered = true;
     return RT_OK;
   }
 
   // launch geometry: persistent grid = resident blocks per CU x CUs
   c->lds = c->img.words.size() <= rt::kLdsSceneMaxWords && !(p->flags & RT_FLAG_GLOBAL_SCENE);
-  const uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
+  uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
   uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
   uint32_t rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
   const uint32_t stack_cap = std::max(c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u);
   size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
+  // one block may declare at most the CU's 160 KiB: a deep per-lane stack first evicts the LDS copy of
+  // the scene (read from HBM instead); if the stack and the minimum colour-stack levels alone do not
+  // fit, the scene is too deep for this kernel (a status, not a failed launch)
+  if (static_cast<size_t>(rc_lds_words) * 4 + stack_bytes > kLdsPerCu - kLdsReserve) return RT_ERR_STACK;
+  if (c->lds && static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes > kLdsPerCu - kLdsReserve) {
+    c->lds = false;
+    scene_lds_words = 0;
+  }
   c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
@@ -362,6 +384,12 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
   hipFunction_t jit_fn = nullptr, jit_probe = nullptr;
   bool jit_lane = false;
+  c->jit_source = RT_JIT_NONE;
+  c->jit_ms = 0.0;
+  auto note_jit = [c](const rt::JitKernels &jk) {
+    c->jit_source = std::max(c->jit_source, jk.source);
+    c->jit_ms += jk.ms;
+  };
   c->used_fold = false;
   if (trav < 0 || trav == RT_TRAV_STATIC) {
     rt::JitKernels jk;
@@ -369,6 +397,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     const bool want_fold = c->fold_enabled && !(p->flags & RT_FLAG_NO_FOLD) &&
                            ray_bound(c->img, cam, p) <= kFoldRayBound;
     if (rt::jit_kernels(c->img, c->variant | trace_bit, c->jit_budget, want_fold, &jk, &why)) {
+      note_jit(jk);
       c->used_fold = jk.folded;
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
@@ -383,6 +412,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     rt::JitKernels jk;
     std::string why;
     if (rt::jit_accel_kernels(c->img, c->variant | trace_bit, &jk, &why)) {
+      note_jit(jk);
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
       jit_lane = true;   // per-lane stacks
@@ -397,6 +427,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     rt::JitKernels jk;
     std::string why;
     if (rt::jit_lane_kernels(c->img, c->variant | trace_bit, &jk, &why)) {
+      note_jit(jk);
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
       jit_lane = true;
@@ -553,7 +584,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->last_cam = *cam;
   c->last_params = *p;
   c->last_out = out_dev;
+  c->last_out8 = out8_dev;
   c->last_stream = stream;
+  c->rendered = true;
   return RT_OK;
 }
 
@@ -569,6 +602,8 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->accel_spheres = c->accel_ok ? static_cast<int32_t>(c->accel.spheres) : 0;
   st->accel_depth = c->accel_ok ? static_cast<int32_t>(c->accel.depth) : 0;
   if (!c->rendered) return RT_OK;
+  st->jit_source = c->jit_source;
+  st->jit_ms = c->jit_ms;
   DeviceGuard g(c->device);
   if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;
   if (c->used_fold) {
@@ -580,7 +615,7 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
       c->fold_violations++;
       rt_params q = c->last_params;
       q.flags |= RT_FLAG_NO_FOLD;
-      const int rc = rt_context_render(c, &c->last_cam, &q, c->last_out, c->last_stream);
+      const int rc = rt_context_render_ppm(c, &c->last_cam, &q, c->last_out, c->last_out8, c->last_stream);
       if (rc != RT_OK) return rc;
       return rt_context_timing(c, st);
     }
@@ -628,9 +663,12 @@ int rt_render(const rt_scene *scene, const rt_camera *cam, const rt_params *p, f
     DeviceGuard g(dev);
     if (bytes && out.ensure(bytes) != hipSuccess) { rt_context_destroy(c); return RT_ERR_HIP; }
     st = rt_context_render(c, cam, p, static_cast<float *>(out.p), nullptr);
+    // rt_context_timing checks the folded traversal's bound flag and re-renders the frame unfolded
+    // when a ray exceeded it: it must run before the copy, stats requested or not
+    rt_stats local{};
+    if (st == RT_OK) st = rt_context_timing(c, stats ? stats : &local);
     if (st == RT_OK && hipDeviceSynchronize() != hipSuccess) st = RT_ERR_HIP;
     if (st == RT_OK && bytes && hipMemcpy(out_rgb, out.p, bytes, hipMemcpyDeviceToHost) != hipSuccess) st = RT_ERR_HIP;
-    if (st == RT_OK && stats) st = rt_context_timing(c, stats);
     out.release();
   }
   rt_context_destroy(c);

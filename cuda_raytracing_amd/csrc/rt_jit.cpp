@@ -3,21 +3,29 @@
 // The render body and the per-node helpers are the same source as the offline kernels
 // (device/rt_body.h, embedded here as text); only the traversal differs.  Compiled with the same
 // numerics flags as the offline build (-ffp-contract=off, correctly rounded f32 div/sqrt), so the
-// frames are bit-identical to the generic kernels'.  Modules are cached per (scene, variant, device).
+// frames are bit-identical to the generic kernels'.  Modules are cached per (scene, variant, device) in
+// the process, and their code objects on disk (cache_dir()) so a new process skips the compile.
 #include "rt_jit.h"
 
 #include <hip/hiprtc.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
-#include <algorithm>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <vector>
 
 #include "device/embedded_headers.inc"
+#include "rt_render.h"
 
 namespace rt {
 namespace {
@@ -124,21 +132,109 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
 
 namespace {
 
+// ---- on-disk code-object cache -------------------------------------------------------------------
+// A fresh process (bin/raytracing, rt_render from a new program) would otherwise pay a hipRTC compile
+// (seconds) per scene/variant.  Entries are keyed by everything the code object depends on: the arch,
+// the hipRTC version, the extra options, the embedded device headers and the generated source.  The
+// full key is stored in the file and compared on load, so a hash collision can only cost a compile.
+// Directory: RT_JIT_CACHE_DIR, else $XDG_CACHE_HOME/cuda_raytracing_amd, else ~/.cache/cuda_raytracing_amd;
+// RT_JIT_CACHE_DIR=0 disables it.
+uint64_t fnv1a(const std::string &s, uint64_t h = 1469598103934665603ull) {
+  for (unsigned char ch : s) { h ^= ch; h *= 1099511628211ull; }
+  return h;
+}
+
+std::string cache_dir() {
+  if (const char *e = std::getenv("RT_JIT_CACHE_DIR")) {
+    if (e[0] == '\0' || (e[0] == '0' && e[1] == '\0')) return "";
+    return e;
+  }
+  if (const char *x = std::getenv("XDG_CACHE_HOME"); x && x[0]) return std::string(x) + "/cuda_raytracing_amd";
+  if (const char *h = std::getenv("HOME"); h && h[0]) return std::string(h) + "/.cache/cuda_raytracing_amd";
+  return "";
+}
+
+bool make_dirs(const std::string &d) {
+  std::string cur;
+  for (size_t i = 0; i <= d.size(); ++i) {
+    if (i == d.size() || d[i] == '/') {
+      if (!cur.empty() && mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST) return false;
+    }
+    if (i < d.size()) cur += d[i];
+  }
+  return true;
+}
+
+constexpr char kCacheMagic[8] = {'R', 'T', 'J', 'I', 'T', 'C', 'O', '1'};
+
+bool disk_load(const std::string &path, const std::string &key, std::vector<char> *code) {
+  FILE *f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  char magic[8];
+  uint64_t klen = 0, clen = 0;
+  bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCacheMagic, 8) == 0 &&
+            std::fread(&klen, 8, 1, f) == 1 && klen == key.size();
+  if (ok) {
+    std::string k(klen, '\0');
+    ok = std::fread(&k[0], 1, klen, f) == klen && k == key && std::fread(&clen, 8, 1, f) == 1 && clen > 0 &&
+         clen < (1ull << 30);
+    if (ok) {
+      code->resize(clen);
+      ok = std::fread(code->data(), 1, clen, f) == clen;
+    }
+  }
+  std::fclose(f);
+  return ok;
+}
+
+void disk_store(const std::string &dir, const std::string &path, const std::string &key, const std::vector<char> &code) {
+  if (!make_dirs(dir)) return;
+  const std::string tmp = path + ".tmp." + std::to_string(static_cast<long>(getpid()));
+  FILE *f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const uint64_t klen = key.size(), clen = code.size();
+  bool ok = std::fwrite(kCacheMagic, 1, 8, f) == 8 && std::fwrite(&klen, 8, 1, f) == 1 &&
+            std::fwrite(key.data(), 1, klen, f) == klen && std::fwrite(&clen, 8, 1, f) == 1 &&
+            std::fwrite(code.data(), 1, clen, f) == clen;
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());   // atomic publish
+}
+
+std::string toolchain_tag() {
+  int major = 0, minor = 0;
+  hiprtcVersion(&major, &minor);
+  static const std::string headers = std::to_string(fnv1a(std::string(kEmbedLayout) + '\x01' + kEmbedBody));
+  return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " headers " + headers;
+}
+
 // Compile (or fetch) the module of `src` exporting <prefix>_render, <prefix>_render_count, <prefix>_probe.
 bool build_module(const std::string &src, const std::string &prefix, JitKernels *out, std::string *why) {
+  const auto t0 = std::chrono::steady_clock::now();
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const std::string arch = arch_of(dev);
-  std::string key = arch + "|" + std::to_string(dev) + "|";
-  for (const std::string &x : jit_extra_options()) key += x + " ";
-  key += "|" + src;
+  std::string opts;
+  for (const std::string &x : jit_extra_options()) opts += x + " ";
+  const std::string disk_key = arch + "|" + toolchain_tag() + "|" + opts + "|" + src;
+  const std::string key = std::to_string(dev) + "|" + disk_key;
   std::lock_guard<std::mutex> lock(g_mu);
+  int source = RT_JIT_MEMORY;
   auto it = g_cache.find(key);
   if (it == g_cache.end()) {
     auto e = std::make_unique<Entry>();
     std::vector<char> code;
     std::string log;
-    if (!jit_compile(src, arch, &code, &log)) {
+    const std::string dir = cache_dir();
+    char name[40];
+    std::snprintf(name, sizeof name, "/rt_%016llx.co", static_cast<unsigned long long>(fnv1a(disk_key)));
+    const std::string path = dir.empty() ? "" : dir + name;
+    bool have = !path.empty() && disk_load(path, disk_key, &code);
+    source = have ? RT_JIT_DISK : RT_JIT_COMPILED;
+    if (!have && jit_compile(src, arch, &code, &log)) {
+      have = true;
+      if (!path.empty()) disk_store(dir, path, disk_key, code);
+    }
+    if (!have) {
       e->why = "hipRTC compile failed: " + log.substr(0, 2000);
     } else if (hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
                hipModuleGetFunction(&e->k.render, e->mod, (prefix + "_render").c_str()) != hipSuccess ||
@@ -159,6 +255,8 @@ bool build_module(const std::string &src, const std::string &prefix, JitKernels 
   *out = it->second->k;
   out->visits = visits;
   out->folded = folded;
+  out->source = source;
+  out->ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return true;
 }
 

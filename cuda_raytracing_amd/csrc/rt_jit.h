@@ -15,6 +15,8 @@ struct JitKernels {
   hipFunction_t probe = nullptr;         // StaticTrace, schedule probe launches (same body, own symbol)
   uint32_t visits = 0;                   // node visits in the expanded traversal
   bool folded = false;                   // primitive tests exactly folded (scene_codegen.cpp)
+  int source = 0;                        // RT_JIT_MEMORY / RT_JIT_DISK / RT_JIT_COMPILED (rt_render.h)
+  double ms = 0.0;                       // host time spent obtaining the module in this call
 };
 
 // Compile (or fetch from the process-wide cache) the StaticTrace kernels of `img` for `variant`

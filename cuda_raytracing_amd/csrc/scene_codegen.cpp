@@ -383,7 +383,14 @@ bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold
     // the host enables folding only when it can bound every ray by 1e6 (camera + scene box + materials);
     // a lane that ever sees a larger or non-finite ray flags the frame, which the host then re-renders
     // without folding (rt_context_timing), so a wrong bound can cost time but never change a frame
-    *src += "    const float kB = 1.0e9f;\n";
+    // RT_FOLD_CHECK_BOUND (tests only) lowers the flag threshold so that a violation can be forced
+    std::string kb = "1.0e9f";
+    if (const char *e = std::getenv("RT_FOLD_CHECK_BOUND")) {
+      char buf[64];
+      std::snprintf(buf, sizeof buf, "%.9gf", std::atof(e));
+      kb = buf;
+    }
+    *src += "    const float kB = " + kb + ";\n";
     *src += "    const bool small = (fabsf(r.o.x) <= kB) & (fabsf(r.o.y) <= kB) & (fabsf(r.o.z) <= kB) &\n";
     *src += "                       (fabsf(r.d.x) <= kB) & (fabsf(r.d.y) <= kB) & (fabsf(r.d.z) <= kB);\n";
     *src += "    if (!small) atomicOr(A.fold_violation, 1u);\n";

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* status codes */
 #define RT_OK                 0
@@ -122,8 +122,15 @@ typedef struct rt_stats {
   int32_t accel_spheres;   /* spheres in the verified traversal's tree (RT_TRAV_ACCEL), else 0 */
   int32_t accel_depth;     /* depth of that tree */
   uint32_t accel_fallbacks; /* rays of the last render the verified traversal re-traced with the reference walk */
-  uint32_t pad_;
+  int32_t jit_source;      /* where the last render's run-time kernels came from: RT_JIT_* below */
+  double jit_ms;           /* host time the last render spent obtaining them (compile or cache load) */
 } rt_stats;
+
+/* rt_stats.jit_source */
+#define RT_JIT_NONE      0   /* offline kernels only */
+#define RT_JIT_MEMORY    1   /* module already loaded in this process */
+#define RT_JIT_DISK      2   /* code object read from the on-disk cache (RT_JIT_CACHE_DIR) */
+#define RT_JIT_COMPILED  3   /* compiled by hipRTC in this call (then written to the disk cache) */
 
 /* One-shot: compile scene, upload, seed RNG, render, copy back.  out_rgb: host buffer of
  * row_count*width*3 floats (linear RGB, already scaled by 1/spp, row-major over the shard's rows).
@@ -143,7 +150,10 @@ int rt_context_render(rt_context *ctx, const rt_camera *camera, const rt_params 
  * finishes it, into out_ppm_device (row_count*width*3 bytes): no separate tonemap pass. */
 int rt_context_render_ppm(rt_context *ctx, const rt_camera *camera, const rt_params *params,
                           float *out_rgb_device, uint8_t *out_ppm_device, void *stream);
-/* Blocks on the last render's events; fills init/render ms, samples and (if counted) counters. */
+/* Blocks on the last render's events; fills init/render ms, samples and (if counted) counters.
+ * If the last rt_context_render* call failed (or none was made) the timings, samples and counters are
+ * left 0: a failed call never reports an earlier frame's events.  A folded frame whose rays exceeded
+ * the host's bound is re-rendered unfolded here (fold_rerenders), into the same float and PPM buffers. */
 int rt_context_timing(rt_context *ctx, rt_stats *stats);
 void rt_context_destroy(rt_context *ctx);
 

@@ -787,3 +787,12 @@ int rt_oracle_threads(void) {
   return 1;
 #endif
 }
+
+/* bench.py's CPU baseline: the same render on n threads (1 = the single-core rate) */
+int rt_oracle_set_threads(int n) {
+  if (n < 1) return RT_ERR_INVALID_ARG;
+#ifdef _OPENMP
+  omp_set_num_threads(n);
+#endif
+  return RT_OK;
+}

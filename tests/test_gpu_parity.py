@@ -533,3 +533,104 @@ def test_random_sphere_worlds_verified_walk(seed):
     fb, st = gpu(w.scene(), cam, p)
     assert st.traversal == rt.RT_TRAV_ACCEL
     assert np.array_equal(bits(fb), bits(ref))
+
+
+# ---- BASELINE configs at their full frame size: strided rows (first and last included) vs the oracle ----
+# (scene, W, H, spp, bounces, row stride): the GPU renders the WHOLE frame (reduced spp), the oracle the
+# rows 0, s, 2s, ..., H-1 of it (the RNG subsequence is the global pixel index, so any row set is
+# comparable); once with the auto policy and once with the forced reference lane walk
+FULL_SIZE_CONFIGS = [
+    (0, 1920, 1080, 4, 16, 83),       # config 2
+    (1, 1920, 1080, 2, 50, 83),       # config 3 (scene 1 as indexed: Cornell box)
+    (17, 1920, 1080, 2, 50, 83),      # config 3 (the Perlin spheres the config names)
+    (20, 1920, 1080, 2, 16, 83),      # config 4 (10k random spheres)
+    (0, 3840, 2160, 1, 50, 127),      # config 5
+]
+
+
+@pytest.mark.parametrize("idx,W,H,spp,b,stride", FULL_SIZE_CONFIGS)
+@pytest.mark.parametrize("force", [0, rt.RT_FLAG_FORCE_LANE])
+def test_full_size_config_rows_match_oracle(idx, W, H, spp, b, stride, force):
+    assert (H - 1) % stride == 0   # the strided rows end on the last row
+    w, s = rt.build_scene(idx)
+    cam, W2, H2 = rt.camera_from_settings(s, W, H)
+    assert (W2, H2) == (W, H)
+    full, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=force))
+    if force:
+        assert st.traversal == rt.RT_TRAV_LANE
+    p = rt.make_params(s, W, H, spp=spp, bounces=b, row_offset=0, row_stride=stride, row_count=(H - 1) // stride + 1)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    got = full[0::stride]
+    assert got.shape == ref.shape
+    bad = np.argwhere(bits(got) != bits(ref))
+    assert bad.size == 0, f"{len(bad)} values differ, first at row {bad[0][0] * stride} col {bad[0][1]}"
+
+
+def test_fold_violation_rerenders_exactly(monkeypatch):
+    # force the folded kernel's ray-bound flag (RT_FOLD_CHECK_BOUND lowers its threshold): rt_render must
+    # re-render unfolded BEFORE copying the frame out, stats or not, and the PPM bytes of the context path
+    # must come from the re-rendered frame too
+    monkeypatch.setenv("RT_FOLD_CHECK_BOUND", "0.25")
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 40, 24)
+    p = rt.make_params(s, W, H, spp=3, bounces=8)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_STATIC and st.fold_rerenders == 1
+    assert np.array_equal(bits(fb), bits(ref))
+    fb2 = rt.render(w.scene(), cam, p)            # no stats requested: the check still runs
+    assert np.array_equal(bits(fb2), bits(ref))
+    ctx = rt.RenderContext(w.scene(), 0)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    out8 = torch.full((H, W, 3), 7, dtype=torch.uint8, device="cuda")
+    ctx.render_into(cam, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream, out8.data_ptr())
+    st = ctx.timing()
+    torch.cuda.synchronize()
+    assert st.fold_rerenders == 1
+    assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
+    assert np.array_equal(out8.cpu().numpy(), rt.tonemap(ref))
+    ctx.close()
+
+
+def test_failed_render_never_reports_stale_timings():
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 32, 18)
+    ctx = rt.RenderContext(w.scene(), 0)
+    out = torch.empty((H, W, 3), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    ctx.render_into(cam, rt.make_params(s, W, H, spp=2, bounces=4), out.data_ptr(), stream)
+    st = ctx.timing()
+    assert st.render_ms > 0 and st.samples == W * H * 2
+    bad = rt.make_params(s, W, H, spp=2, bounces=4)
+    bad.row_stride = 0
+    with pytest.raises(rt.RenderError):
+        ctx.render_into(cam, bad, out.data_ptr(), stream)
+    st = ctx.timing()
+    assert st.render_ms == 0 and st.samples == 0 and st.init_ms == 0
+    ctx.render_into(cam, rt.make_params(s, W, H, spp=2, bounces=4), out.data_ptr(), stream)
+    assert ctx.timing().samples == W * H * 2
+    ctx.close()
+
+
+def test_code_object_disk_cache(tmp_path):
+    # a second process finds the scene-specialised kernels on disk (no hipRTC compile) and writes the
+    # same PPM bytes; the CLI reports the end-to-end time of the whole reference render() region
+    import os
+    import subprocess
+    from conftest import REPO
+    exe = REPO / "bin" / "raytracing"
+    env = dict(os.environ, RT_JIT_CACHE_DIR=str(tmp_path / "cache"))
+    outs = []
+    for k in range(2):
+        d = tmp_path / f"run{k}"
+        d.mkdir()
+        r = subprocess.run([str(exe), "0", "s2", "b4", "w64", "h36"], cwd=d, capture_output=True, text=True,
+                           timeout=180, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs.append((r.stdout, b"".join(f.read_bytes() for f in sorted(d.glob("*.ppm")))))
+    assert "[compiled" in outs[0][0] and "[disk cache" in outs[1][0], (outs[0][0], outs[1][0])
+    assert "End-to-end:" in outs[1][0]
+    assert outs[0][1] and outs[0][1] == outs[1][1]
+    assert list((tmp_path / "cache").glob("rt_*.co"))

@@ -13,13 +13,13 @@ step() {  # name, limit, command...
 }
 SKIP_TESTS=${SKIP_TESTS:-0}
 if [ "$SKIP_TESTS" != 1 ]; then
-  step pytest_gpu 900 python3 -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread
+  step pytest_gpu 900 python3 -u -m pytest tests -v -m gpu --timeout 180 --timeout-method thread ${PYTEST_ARGS:-}
   step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 fi
 step bench 900 python3 bench.py ${BENCH_ARGS:-}
 if [ "${PROFILE:-1}" = 1 ]; then
   export TMPDIR=/tmp
-  step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 3 --warmup 1 --inflight 1 --no-cpu-baseline
+  step rocprof_stats 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o run -- python3 bench.py --steps 3 --warmup 1 --pipelined-steps 0 --no-cpu-baseline --no-e2e ${BENCH_ARGS:-}
 fi
 if [ "${PMC:-0}" = 1 ]; then
   step pmc 1000 python3 tools/profile_pmc.py --out "$PWD/gpurun_out/pmc" ${PMC_ARGS:---scene 0 --spp 512}
