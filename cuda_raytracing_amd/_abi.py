@@ -167,7 +167,7 @@ def host_lib():
 HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_render_ppm", "rt_context_timing",
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
-               "rt_seed_states"]
+               "rt_seed_states", "rt_kernel_source"]
 
 
 def _bind_single_hip_runtime():
@@ -212,6 +212,7 @@ def hip_lib():
         _sig(L.rt_tonemap_device, C.c_int, P, C.c_uint64, P, P)
         _sig(L.rt_accel_build, C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
         _sig(L.rt_seed_states, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
+        _sig(L.rt_kernel_source, C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.c_char_p, C.c_uint64)
         _hip = L
     return _hip
 

@@ -331,9 +331,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->counted = (p->flags & RT_FLAG_COUNT) != 0;
   c->samples = static_cast<uint64_t>(n) * static_cast<uint64_t>(p->samples_per_pixel);
   c->used_fold = false;
-  if (n == 0) {
-    for (hipEvent_t e : c->ev)
-      if (hipEventRecord(e, s) != hipSuccess) return RT_ERR_HIP;
+  if (n == 0) {   // same event order as a render: seed | schedule | render, ev[2] (render end) last
+    for (int k : {0, 1, 3, 2})
+      if (hipEventRecord(c->ev[k], s) != hipSuccess) return RT_ERR_HIP;
     c->rendered = true;
     return RT_OK;
   }
@@ -716,6 +716,34 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
   const bool ok = rt::jit_compile(src, arch, &code, &lg);
   copy_out(lg, log, cap);
   return ok ? RT_OK : RT_ERR_HIP;
+}
+
+int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap) {
+  if (!scene || !buf || cap == 0) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  int rc = rt::compile_scene(scene, &img);
+  if (rc != RT_OK) return rc;
+  while (img.words.size() % 4) img.words.push_back(0);
+  const uint32_t mb = static_cast<uint8_t>(max_bounces);
+  const int variant = (img.words.size() <= rt::kLdsSceneMaxWords ? rt::kVarLds : 0) | (img.has_noise ? rt::kVarNoise : 0) |
+                      (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img) |
+                      (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0);
+  std::string src;
+  if (traversal == RT_TRAV_STATIC) {
+    uint32_t v = 0;
+    if (!rt::jit_source(img, variant, 256, true, &src, &v)) return RT_ERR_UNSUPPORTED;
+  } else if (traversal == RT_TRAV_ACCEL) {
+    rt::SphereAccel a;
+    std::string why;
+    if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
+    src = rt::jit_accel_source(img, variant);
+  } else if (traversal == RT_TRAV_LANE) {
+    src = rt::jit_lane_source(img, variant);
+  } else {
+    return RT_ERR_INVALID_ARG;
+  }
+  copy_out(src, buf, cap);
+  return RT_OK;
 }
 
 int rt_tonemap_device(const float *rgb, uint64_t pixels, uint8_t *out, void *stream) {

@@ -169,6 +169,10 @@ int rt_tonemap_device(const float *rgb_device, uint64_t pixels, uint8_t *out_dev
  * rt_static_compile: compiles that source for `arch` (e.g. "gfx950"); the compiler log goes to log. */
 int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint64_t cap, uint32_t *visits);
 int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *arch, char *log, uint64_t cap);
+/* The run-time (hipRTC) source of any traversal's kernels for `scene` as a render with max_bounces
+ * would build it (traversal = RT_TRAV_STATIC, RT_TRAV_ACCEL or RT_TRAV_LANE; no device needed):
+ * ISA / register / scratch inspection with hipcc (tools/isa_stats.sh). */
+int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap);
 /* Diagnostics for the verified sphere traversal (no device needed): builds the SAH tree of an
  * all-sphere world.  info = {root node, depth, spheres, node words}; words (if non-null, cap words)
  * receives the node words then the prim words (layout: device/rt_layout.h kAccel*).
