@@ -319,6 +319,88 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
 }
 
 // ---------------------------------------------------------------------------------------------
+// compact colour stack (rt_layout.h kRcRecTag): a level holds a code of its attenuation
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rc_rec(uint32_t r, bool wide) { return wide ? (kRcRecTag | r) : r; }
+
+// texture_color's resolution (checker recursion, image clamp, noise) returning the colour-stack code of
+// the Lambertian attenuation instead of the colour: rc_decode(code) == texture_color(...) bit for bit
+template <bool LDS, bool COUNT, bool NOISE, bool UV, uint32_t TM, bool WIDE>
+__device__ uint32_t texture_code(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti, float u, float v, f3 p,
+                                 uint32_t &perlin_count) {
+  if (TM == (1u << T_SOLID)) return rc_rec(A.rc_tex0 + ti, WIDE);   // solid colours only: no load
+  for (int guard = 0; guard < 64; ++guard) {
+    const uint32_t b = A.off_texs + ti * kTexWords;
+    const uint4 t0 = S.w4(b);
+    if (!(TM & (1u << T_CHECKER)) && !(TM & (1u << T_IMAGE)) && !(TM & (1u << T_NOISE)))
+      return rc_rec(A.rc_tex0 + ti, WIDE);
+    switch (t0.x) {
+      case T_SOLID:
+        return rc_rec(A.rc_tex0 + ti, WIDE);
+      case T_CHECKER: {
+        if (!(TM & (1u << T_CHECKER))) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
+        float inv = asf(t0.w);
+        int32_t x = static_cast<int32_t>(floorf(inv * p.x));
+        int32_t y = static_cast<int32_t>(floorf(inv * p.y));
+        int32_t z = static_cast<int32_t>(floorf(inv * p.z));
+        bool even = ((x + y + z) & 1) == 0;
+        ti = even ? t0.y : t0.z;
+      } break;
+      case T_IMAGE: {
+        if (!(TM & (1u << T_IMAGE))) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
+        if (!UV) return rc_rec(A.rc_consts + RC_MAGENTA, WIDE);   // no pixels anywhere (host-checked)
+        uint4 t1 = S.w4(b + 4);
+        if (t1.x == 0) return rc_rec(A.rc_consts + RC_MAGENTA, WIDE);
+        int32_t wd = static_cast<int32_t>(t0.y), ht = static_cast<int32_t>(t0.z);
+        float cu = (u < 0) ? 0 : ((u > 1) ? 1 : u);
+        float cv = 1.0f - ((v < 0) ? 0 : ((v > 1) ? 1 : v));
+        int32_t x = static_cast<int32_t>(cu * wd), y = static_cast<int32_t>(cv * ht);
+        x = (x < 0) ? 0 : ((x > wd) ? wd : x);
+        y = (y < 0) ? 0 : ((y > ht) ? ht : y);
+        uint64_t wo = static_cast<uint64_t>(t0.w) + 3ull * (static_cast<uint64_t>(y) * wd + x);
+        if (wo + 3 > A.pixel_words) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
+        return kRcTexelTag | static_cast<uint32_t>(wo);   // UV kernels are wide; pixel pool < 2^23 words
+      }
+      case T_NOISE: {
+        if (!NOISE || !(TM & (1u << T_NOISE))) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
+        if (COUNT) perlin_count++;
+        const uint32_t tb = A.off_perlin + t0.y * kPerlinWords;
+        float accum = 0.0f, weight = 1.0f;
+        f3 q = p;
+#pragma unroll
+        for (int oct = 0; oct < 7; ++oct) {
+          accum += weight * perlin_noise(S, tb, q);
+          weight *= 0.5f;
+          q = mk(q.x * 2, q.y * 2, q.z * 2);
+        }
+        float turb = fabsf(accum);
+        float s = 1 + rt_sinf(asf(t0.w) * p.z + 10 * turb);
+        const uint32_t g = __float_as_uint(0.5f * s);   // attenuation (g, g, g); NOISE kernels are wide
+        return ((g & kRcRecTag) == kRcRecTag) ? (kRcRecTag | (A.rc_consts + RC_NAN)) : g;
+      }
+      default:
+        return rc_rec(A.rc_consts + RC_BLACK, WIDE);
+    }
+  }
+  return rc_rec(A.rc_consts + RC_BLACK, WIDE);
+}
+
+// code -> attenuation (the record's words 1..3, the texel, or the grey)
+template <bool LDS, bool WIDE, bool NOISE, bool UV>
+__device__ __forceinline__ f3 rc_decode(const Mem<LDS> &S, const RenderArgs &A, uint32_t w) {
+  const bool grey = NOISE && (w & kRcRecTag) != kRcRecTag;   // a grey reads record 0 (in bounds), unused
+  if (!WIDE || !UV) {
+    const uint32_t r = grey ? 0u : (WIDE ? (w & kRcPayload) : w);
+    const uint4 q = S.w4(A.off_mats + r * kRecWords);
+    return grey ? mk(asf(w), asf(w), asf(w)) : mk(asf(q.y), asf(q.z), asf(q.w));
+  }
+  const bool texel = (w & kRcTexelTag) == kRcTexelTag;
+  const uint32_t o = grey ? A.off_mats : (texel ? A.off_pixels + (w & kRcPayload) : A.off_mats + (w & kRcPayload) * kRecWords + 1);
+  const f3 c = mk(S.f(o), S.f(o + 1), S.f(o + 2));
+  return grey ? mk(asf(w), asf(w), asf(w)) : c;
+}
+
+// ---------------------------------------------------------------------------------------------
 // traversal state and the per-node operations of hit() (raytracing.cu:1079-1251)
 // ---------------------------------------------------------------------------------------------
 struct Ray { f3 o, d; float time; };
@@ -938,11 +1020,30 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   }
   const uint32_t lane = __lane_id();
   const uint32_t wave = threadIdx.x >> 6;
-  uint16_t *stk = reinterpret_cast<uint16_t *>(g_lds + A.stack_lds_word) + wave * A.stack_cap * 64 + lane;
-  // colour stack: level k channel c at rc_l[(3k + c) * 64] (lane-interleaved, conflict-free) for
-  // k < rc_lds_levels, else in HBM at rc[(3k + c) * threads + gtid]
-  float *rc_l = reinterpret_cast<float *>(g_lds + A.rc_lds_word) + wave * A.rc_lds_levels * 192 + lane;
   const uint32_t gtid = blockIdx.x * kBlock + threadIdx.x;
+  uint16_t *stk = reinterpret_cast<uint16_t *>(g_lds + A.stack_lds_word) + wave * A.stack_cap * 64 + lane;
+  // colour stack (codes, rt_layout.h): level k < rc_lds_levels in LDS, lane-interleaved (conflict-free) —
+  // wide: rcw[k * 64]; narrow: two levels per word, rch[(k >> 1) * 128 + (k & 1)] (rc_lds_levels even) —
+  // deeper levels in HBM at rc[k * threads + gtid]
+  constexpr bool WIDE = (F & kVarNarrow) == 0;
+  uint32_t *rcw = g_lds + A.rc_lds_word + wave * A.rc_lds_levels * 64 + lane;
+  uint16_t *rch = reinterpret_cast<uint16_t *>(g_lds + A.rc_lds_word + wave * (A.rc_lds_levels >> 1) * 64 + lane);
+  auto rc_lds_store = [&](uint32_t k, uint32_t code) {
+    if (WIDE) rcw[k * 64] = code;
+    else rch[(k >> 1) * 128 + (k & 1)] = static_cast<uint16_t>(code);
+  };
+  auto rc_lds_load = [&](uint32_t k) -> uint32_t {
+    return WIDE ? rcw[k * 64] : static_cast<uint32_t>(rch[(k >> 1) * 128 + (k & 1)]);
+  };
+  auto rc_hbm_store = [&](uint32_t k, uint32_t code) {
+    const size_t i = static_cast<size_t>(k) * A.threads + gtid;
+    if (WIDE) static_cast<uint32_t *>(A.rc)[i] = code;
+    else static_cast<uint16_t *>(A.rc)[i] = static_cast<uint16_t>(code);
+  };
+  auto rc_hbm_load = [&](uint32_t k) -> uint32_t {
+    const size_t i = static_cast<size_t>(k) * A.threads + gtid;
+    return WIDE ? static_cast<const uint32_t *>(A.rc)[i] : static_cast<uint32_t>(static_cast<const uint16_t *>(A.rc)[i]);
+  };
   const uint64_t lt_mask = (1ull << lane) - 1ull;
   const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
 
@@ -950,7 +1051,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool hot = false;                       // the pixel is one of the first A.prio_ids handed out
   bool raised = false;                    // wave-uniform: s_setprio raised
   int32_t pix = 0, sample = 0;
-  uint32_t depth = 0;
+  uint32_t depth = 0;                     // bounces of the current path (max_bounces, :1336)
+  uint32_t rsp = 0;                       // colour-stack levels pushed (dielectric bounces push none)
   Rng rng{0, 0, 0, 0, 0, 0};
   Ray ray;
   ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
@@ -1003,6 +1105,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     ray.d = add(ray.d, scale(yo, mk(A.dv[0], A.dv[1], A.dv[2])));
     ray.time = rng.uniform();
     depth = 0;
+    rsp = 0;
   };
 
   for (;;) {
@@ -1055,9 +1158,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             rng.d = hsh; rng.x0 = hsh ^ 0x2c7f967fu; rng.x1 = hsh * 3u + 1u; rng.x2 = ~hsh;
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
           } else {
-            const uint32_t n = A.n_pixels;
-            rng.d = A.rng[pix]; rng.x0 = A.rng[n + pix]; rng.x1 = A.rng[2 * n + pix];
-            rng.x2 = A.rng[3 * n + pix]; rng.x3 = A.rng[4 * n + pix]; rng.x4 = A.rng[5 * n + pix];
+            // tile-major states: the wave's lanes read consecutive words (256 B per state word)
+            const uint32_t n = A.n_ids, ri = tile * 64u + k;
+            rng.d = A.rng[ri]; rng.x0 = A.rng[n + ri]; rng.x1 = A.rng[2 * n + ri];
+            rng.x2 = A.rng[3 * n + ri]; rng.x3 = A.rng[4 * n + ri]; rng.x4 = A.rng[5 * n + ri];
           }
           sum = mk(0, 0, 0);
           sample = 0;
@@ -1157,22 +1261,25 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         emit = texture_color<LDS, COUNT, NOISE, UV, TM>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
       ruv = scale(1.0f / length(ruv), ruv);
       bool scattered = false;
-      f3 dir = mk(0, 0, 0), att = mk(0, 0, 0);
+      bool push = false;        // dielectrics push no level: their attenuation (1,1,1) is x*1 == x
+      uint32_t code = 0;        // colour-stack code of the attenuation (rt_layout.h)
+      f3 dir = mk(0, 0, 0);
       const bool hfront = hit_front(h);
       const f3 hn = hfront ? h.n : flip(h.n);
       if ((MM & (1u << MAT_LAMBERTIAN)) && mkind == MAT_LAMBERTIAN) {      // :458-465
         scattered = true;
+        push = true;
         dir = add(hn, ruv);
         const float eps = 1e-8f;
         if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = hn;
-        att = texture_color<LDS, COUNT, NOISE, UV, TM>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
+        code = texture_code<LDS, COUNT, NOISE, UV, TM, WIDE>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
       } else if ((MM & (1u << MAT_METAL)) && mkind == MAT_METAL) {         // :466-472
         f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, hn), hn));
         dir = add(unit(rd), scale(asf(m1.y), ruv));
-        att = mk(asf(m0.z), asf(m0.w), asf(m1.x));
+        code = rc_rec(h.mat, WIDE);                                         // albedo: the material record
         scattered = dot(dir, hn) > 0;
+        push = true;
       } else if ((MM & (1u << MAT_DIELECTRIC)) && mkind == MAT_DIELECTRIC) {   // :473-487
-        att = mk(1.0f, 1.0f, 1.0f);
         const float ior = asf(m1.z);
         const float ri = hfront ? (1.0f / ior) : ior;
         const f3 ud = unit(ray.d);
@@ -1196,18 +1303,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         scattered = true;
       }
       if (scattered) {
-        // push attenuation (the emission pushed with it is always 0: only lights emit and lights
-        // never scatter, raytracing.cu:439-450 vs :457-488), so the unwind adds +0.0f per level
-        if (depth < A.rc_lds_levels) {
-          float *slot = rc_l + depth * 192;
-          slot[0] = att.x;
-          slot[64] = att.y;
-          slot[128] = att.z;
-        } else {
-          float *slot = A.rc + (static_cast<size_t>(depth) * 3) * A.threads + gtid;
-          slot[0] = att.x;
-          slot[A.threads] = att.y;
-          slot[2 * static_cast<size_t>(A.threads)] = att.z;
+        // push the attenuation's code (the emission pushed with it is always 0: only lights emit and
+        // lights never scatter, raytracing.cu:439-450 vs :457-488, so the unwind adds +0.0f per level)
+        if (push) {
+          if (rsp < A.rc_lds_levels) rc_lds_store(rsp, code);
+          else rc_hbm_store(rsp, code);
+          rsp++;
         }
         depth++;
         if (COUNT) c_bounce++;
@@ -1230,48 +1331,42 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     if (done) {
       // res = att_k * res + 0.0f from the deepest level (:1362-1368).  With res = (+-0,+-0,+-0) and
       // finite attenuations every level yields +0, so such paths (absorbed, depth-exhausted, escaped
-      // into a black background) skip the stack reads; depth 0 keeps res itself
-      if (A.black_skip && depth > 0 && res.x == 0.0f && res.y == 0.0f && res.z == 0.0f) {
+      // into a black background) skip the stack reads; depth 0 keeps res itself.
+      // The "+ 0.0f" of each level only turns a -0 into +0 (an underflowed product stays +-0 in every
+      // later level) and sum = +0 + ... is never -0, so it is dropped (the pixel is bit-identical); the
+      // same argument covers the dielectric levels, which are not pushed (att (1,1,1)).
+      if (A.black_skip && rsp > 0 && res.x == 0.0f && res.y == 0.0f && res.z == 0.0f) {
         res = mk(0.0f, 0.0f, 0.0f);
-        depth = 0;
+        rsp = 0;
       }
-      // :1362-1368.  Levels past the LDS ones live in HBM/L2: their loads are issued kUnwindBatch at a
-      // time ahead of the multiply chain (one memory latency per batch, not per level — a deep path
-      // otherwise holds its whole wave for hundreds of cycles per level)
-      int32_t k = static_cast<int32_t>(depth) - 1;
+      // Levels past the LDS ones live in HBM/L2: their codes are loaded kUnwindBatch at a time, then
+      // decoded together, ahead of the multiply chain (one memory latency per batch, not per level)
+      int32_t k = static_cast<int32_t>(rsp) - 1;
       const int32_t kl = static_cast<int32_t>(A.rc_lds_levels);
-      while (DEEP && k >= kl) {
-        constexpr int kUnwindBatch = RT_UNWIND_BATCH;
+      while (k >= kl) {
+        constexpr int kUnwindBatch = DEEP ? RT_UNWIND_BATCH : 1;
+        uint32_t cw[kUnwindBatch];
+#pragma unroll
+        for (int i = 0; i < kUnwindBatch; ++i) cw[i] = rc_hbm_load(static_cast<uint32_t>(max(k - i, kl)));
         f3 at[kUnwindBatch];
 #pragma unroll
-        for (int i = 0; i < kUnwindBatch; ++i) {
-          if (k - i >= kl) {
-            const float *slot = A.rc + (static_cast<size_t>(k - i) * 3) * A.threads + gtid;
-            at[i] = mk(slot[0], slot[A.threads], slot[2 * static_cast<size_t>(A.threads)]);
-          }
-        }
+        for (int i = 0; i < kUnwindBatch; ++i) at[i] = rc_decode<LDS, WIDE, NOISE, UV>(S, A, cw[i]);
 #pragma unroll
-        for (int i = 0; i < kUnwindBatch; ++i) {
-          if (k - i >= kl) res = mk(at[i].x * res.x + 0.0f, at[i].y * res.y + 0.0f, at[i].z * res.z + 0.0f);
-        }
+        for (int i = 0; i < kUnwindBatch; ++i)
+          if (k - i >= kl) res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
         k -= kUnwindBatch;
         if (k < kl) k = kl - 1;   // continue with the deepest LDS level
       }
-      for (; !DEEP && k >= kl; --k) {   // shallow kernels: HBM levels are rare, one at a time
-        const float *slot = A.rc + (static_cast<size_t>(k) * 3) * A.threads + gtid;
-        res = mk(slot[0] * res.x + 0.0f, slot[A.threads] * res.y + 0.0f, slot[2 * static_cast<size_t>(A.threads)] * res.z + 0.0f);
-      }
-      // LDS levels, RT_UNWIND_LDS at a time: the loads of a batch are issued together (one LDS latency
-      // per batch, not per level).  Levels below 0 read level 0 and multiply by 1.0f instead (exact).
-      // The "+ 0.0f" of each level only turns a -0 into +0 (an underflowed product stays +-0 in every
-      // later level) and sum = +0 + ... is never -0, so dropping it leaves the pixel bit-identical.
+      // LDS levels, RT_UNWIND_LDS at a time: the code loads of a batch are issued together, then their
+      // decodes (one LDS latency each per batch, not per level).  Levels below 0 read level 0 and
+      // multiply by 1.0f instead (exact).
       for (; k >= 0; k -= RT_UNWIND_LDS) {
+        uint32_t cw[RT_UNWIND_LDS];
+#pragma unroll
+        for (int i = 0; i < RT_UNWIND_LDS; ++i) cw[i] = rc_lds_load(static_cast<uint32_t>(max(k - i, 0)));
         f3 at[RT_UNWIND_LDS];
 #pragma unroll
-        for (int i = 0; i < RT_UNWIND_LDS; ++i) {
-          const float *slot = rc_l + max(k - i, 0) * 192;
-          at[i] = mk(slot[0], slot[64], slot[128]);
-        }
+        for (int i = 0; i < RT_UNWIND_LDS; ++i) at[i] = rc_decode<LDS, WIDE, NOISE, UV>(S, A, cw[i]);
 #pragma unroll
         for (int i = 0; i < RT_UNWIND_LDS; ++i) {
           if (k - i < 0) at[i] = mk(1.0f, 1.0f, 1.0f);

@@ -39,13 +39,28 @@ constexpr uint32_t kAccelLeaf = 0x80000000u;
 constexpr float kAccelKappa = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24): cone padding per unit of |oc|
 enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
 
-// materials (raytracing.cu:78-99): 8 words; kinds == RTR_MAT_* (rt_ref_layout.h)
+// materials (raytracing.cu:78-99): 8 words; kinds == RTR_MAT_* (rt_ref_layout.h).  A metal's albedo
+// sits at words 1..3 like a solid texture's colour (M_TEX is only used by Lambertian / light kinds), so
+// both are "colour records" the compact colour stack can point at (see kRecWords below).
 constexpr int kMatWords = 8;
-enum : int { M_KIND = 0, M_TEX = 1, M_ALBEDO = 2, M_FUZZ = 5, M_IOR = 6 };
+enum : int { M_KIND = 0, M_TEX = 1, M_ALBEDO = 1, M_FUZZ = 5, M_IOR = 6 };
 enum : uint32_t { MAT_LAMBERTIAN = 0, MAT_METAL = 1, MAT_DIELECTRIC = 2, MAT_DIFFUSE_LIGHT = 3 };
 
 // textures (raytracing.cu:38-54): 8 words
 constexpr int kTexWords = 8;
+
+// Colour records: materials, then textures, then kRcConsts constant records, contiguous from
+// off_mats, 8 words each, an attenuation colour (when the record has one) at words 1..3.  Record r
+// starts at word off_mats + 8 r.  Constants: the magenta and black of image_texture_get_pixel /
+// texture_get_color (raytracing.cu:346-347, 397) and a NaN grey (a noise value that is not finite).
+constexpr int kRecWords = 8;
+enum : uint32_t { RC_MAGENTA = 0, RC_BLACK = 1, RC_NAN = 2, kRcConsts = 3 };
+// Colour-stack codes (ray_color's attenuation stack, :1253-1276).  Every attenuation the reference
+// pushes is a record's colour, a texel, or a noise grey (r = g = b); a level stores a code for it:
+//   wide (32 bit):  grey float bits (finite) | kRcRecTag + record | kRcTexelTag + texel word offset
+//   narrow (16 bit, scenes without noise and texels and < 65536 records): the record index
+constexpr uint32_t kRcRecTag = 0x7F800000u, kRcTexelTag = 0xFF800000u, kRcPayload = 0x007FFFFFu;
+static_assert(kMatWords == kRecWords && kTexWords == kRecWords, "colour records are 8 words");
 enum : uint32_t { T_SOLID = 0, T_CHECKER = 1, T_IMAGE = 2, T_NOISE = 3 };
 enum : int {
   T_KIND = 0,
@@ -81,6 +96,12 @@ constexpr int kVarMatShift = 6, kVarTexShift = 10;
 // unwound with batched loads (costs registers, so shallow renders keep the plain loop)
 constexpr int kVarDeep = 1 << 14;
 constexpr int kDeepBounces = 16;
+// run-time compiled kernels whose colour-stack codes fit 16 bits (no noise, no texels, < 65536 colour
+// records): two levels per LDS word.  The offline kernels always use 32-bit codes.
+constexpr int kVarNarrow = 1 << 15;
+// variant bits the run-time compiled kernels are specialised on
+constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | (15 << kVarMatShift) |
+                            (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
@@ -103,6 +124,7 @@ struct RenderArgs {
   uint32_t off_mats, off_texs, off_perlin, off_pixels, pixel_words;
   uint32_t root, stack_cap, stack_lds_word;   // per-lane stack region starts at this LDS word
   uint32_t rc_lds_word, rc_lds_levels;        // colour-stack levels [0, rc_lds_levels) live in LDS
+  uint32_t rc_tex0, rc_consts;                // colour records: first texture, first constant
   // camera (rt_camera)
   float p00[3], du[3], dv[3], center[3], dfu[3], dfv[3], defocus_angle;
   int32_t width, row_offset, row_stride;
@@ -113,10 +135,12 @@ struct RenderArgs {
   uint32_t rows;              // row_count
   uint32_t tiles_x;           // ceil(width / 8)
   uint32_t n_ids;             // 64 * ceil(rows/8) * tiles_x: tile-major pixel ids handed to waves
-  const uint32_t *rng;        // [6][n_pixels] seeded XORWOW states {d, x0..x4}
+  const uint32_t *rng;        // [6][n_ids] seeded XORWOW states {d, x0..x4}, tile-major (tile * 64 + k,
+                              // k = 8 * row-in-tile + column-in-tile): a wave's 64 pixels are 256 B per word
   float *out;                 // [n_pixels][3]
   uint8_t *out8;              // optional [n_pixels][3] P6 payload bytes (pixels_to_ppm), null = none
-  float *rc;                  // attenuation stack: [max_bounces][3][threads]
+  void *rc;                   // colour-stack levels past the LDS ones: [max_bounces][threads] codes
+                              // (u32, or u16 in narrow kernels)
   uint32_t threads;           // grid size in threads (rc stride)
   uint32_t *work;             // chunk counter (zeroed per launch)
   unsigned long long *counters;   // CNT_SLOTS (counting variants only)
@@ -149,9 +173,11 @@ struct SeedArgs {
   const uint32_t *jump;       // xorwow_jump_tables() on device
   uint32_t base[6];           // rocRAND constant seeding of `seed`
   int32_t width, row_offset, row_stride;
-  uint32_t n_pixels;
-  uint32_t per_thread;
-  uint32_t *rng;              // [6][n_pixels]
+  uint32_t rows;              // local rows of the shard
+  uint32_t tiles_x;           // ceil(width / 8)
+  uint32_t n_ids;             // 64 * ceil(rows / 8) * tiles_x (stride between the six state words)
+  uint32_t *rng;              // [6][n_ids], tile-major (RenderArgs::rng)
 };
+constexpr uint32_t kSeedRun = 16;   // consecutive pixels of a row seeded per thread (one jump, then steps)
 
 }  // namespace rt

@@ -16,9 +16,10 @@
 namespace rt {
 
 struct SceneImage {
-  // one contiguous word image: [nodes | mats | texs | perlin | image pixels]
+  // one contiguous word image: [nodes | mats | texs | constant colour records | perlin | image pixels]
   std::vector<uint32_t> words;
   uint32_t node_count = 0, mat_count = 0, tex_count = 0, perlin_count = 0;
+  uint32_t rec_consts = 0;      // colour-record index of the first constant (= mat_count + tex_count)
   uint32_t off_mats = 0, off_texs = 0, off_perlin = 0, off_pixels = 0;   // word offsets
   uint32_t root = 0;            // root record index (already resolved through the ref list)
   uint32_t stack_need = 0;      // exact worst-case hit-stack depth

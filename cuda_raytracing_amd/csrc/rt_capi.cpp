@@ -72,7 +72,10 @@ constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
-constexpr uint32_t kRcLdsMaxLevels = 64;   // colour-stack levels kept in LDS at most
+constexpr uint32_t kRcLdsMaxLevels = 256;  // colour-stack levels kept in LDS at most (max_bounces is a u8)
+
+// LDS bytes of one colour-stack level for a 256-thread block: 32-bit codes, or 16-bit in narrow kernels
+constexpr size_t rc_level_bytes(bool narrow) { return static_cast<size_t>(rt::kWavesPerBlock) * 64 * (narrow ? 2 : 4); }
 
 // Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
 // precondition, scene_codegen.cpp).  Primary rays: camera centre + lens offset, directions to the
@@ -161,7 +164,6 @@ struct rt_context {
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
-  uint32_t seed_per_thread = 16;                // RT_SEED_PER_THREAD: consecutive pixels per seeding thread (0.23 ms at 1080p; 64: 0.27)
   uint32_t defer_lanes = 4;                     // RT_DEFER_LANES: end a round's rejection at <= this many lanes
   uint32_t defer_trace = 16, trace_min_iters = 16;  // RT_DEFER_TRACE, RT_TRACE_MIN (paused per-lane walks)
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
@@ -267,7 +269,6 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
-  if (const char *e = std::getenv("RT_SEED_PER_THREAD")) c->seed_per_thread = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_TRACE")) c->defer_trace = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
@@ -289,6 +290,12 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   // per-lane u16 stacks of 4 waves x 64 lanes: 512 B per entry; 256 entries (128 KiB) plus the minimum
   // colour-stack levels is what one 160 KiB block can hold (checked again per render)
   if (c->img.stack_need > 256) { delete c; return RT_ERR_STACK; }
+  // colour-stack codes carry a record index or a texel word offset in 23 bits (rt_layout.h)
+  if (c->img.rec_consts + rt::kRcConsts > rt::kRcPayload ||
+      (c->img.needs_uv && c->img.words.size() - c->img.off_pixels > rt::kRcPayload)) {
+    delete c;
+    return RT_ERR_UNSUPPORTED;
+  }
   c->black_skip = attenuations_finite(c->img);
   if (const char *e = std::getenv("RT_BLACK_SKIP")) c->black_skip = c->black_skip && e[0] != '0';
   DeviceGuard g(device);
@@ -351,25 +358,29 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // launch geometry: persistent grid = resident blocks per CU x CUs
   c->lds = c->img.words.size() <= rt::kLdsSceneMaxWords && !(p->flags & RT_FLAG_GLOBAL_SCENE);
   uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
+  // colour stack: 16-bit codes in run-time compiled kernels of scenes without noise and texels (and with
+  // < 65536 colour records), 32-bit otherwise; the LDS-scene decision is made with the wide size
+  const bool narrow_ok = !c->img.has_noise && !c->img.needs_uv && c->img.rec_consts + rt::kRcConsts <= 65536u;
   uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
-  uint32_t rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
+  size_t rc_bytes = rc_levels * rc_level_bytes(false);
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
   const uint32_t stack_cap = std::max(c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u);
   size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
   // one block may declare at most the CU's 160 KiB: a deep per-lane stack first evicts the LDS copy of
   // the scene (read from HBM instead); if the stack and the minimum colour-stack levels alone do not
   // fit, the scene is too deep for this kernel (a status, not a failed launch)
-  if (static_cast<size_t>(rc_lds_words) * 4 + stack_bytes > kLdsPerCu - kLdsReserve) return RT_ERR_STACK;
-  if (c->lds && static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes > kLdsPerCu - kLdsReserve) {
+  if (rc_bytes + stack_bytes > kLdsPerCu - kLdsReserve) return RT_ERR_STACK;
+  if (c->lds && static_cast<size_t>(scene_lds_words) * 4 + rc_bytes + stack_bytes > kLdsPerCu - kLdsReserve) {
     c->lds = false;
     scene_lds_words = 0;
   }
-  c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4 + stack_bytes;
+  c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + rc_bytes + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
-                        (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0);
+                        (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
+                        (narrow_ok ? rt::kVarNarrow : 0);
   // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
   // at most jit_budget node visits (every catalog scene but the large random ones), else the per-lane
   // DFS.  The wave-packet DFS is kept as an explicit option (fastest on tiny all-sphere scenes).
@@ -436,10 +447,11 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     }
   }
   if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
-  if (jit_fn && !jit_lane) {   // straight-line traversal: no stacks
-    stack_bytes = 0;
-    c->lds_bytes = static_cast<size_t>(scene_lds_words + rc_lds_words) * 4;
-  }
+  if (jit_fn && !jit_lane) stack_bytes = 0;   // straight-line traversal: no stacks
+  const bool narrow = jit_fn != nullptr && narrow_ok;   // the offline kernels use 32-bit codes
+  const size_t level_bytes = rc_level_bytes(narrow);
+  if (narrow) rc_levels = (rc_levels + 1) & ~1u;        // two levels per LDS word
+  c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + rc_levels * level_bytes + stack_bytes;
   c->used_traversal = trav;
   int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes) : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
   if (c->blocks_per_cu > 0) per_cu = std::min(c->blocks_per_cu, per_cu);   // fewer blocks: more LDS levels each
@@ -448,24 +460,24 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     // touch HBM), without lowering residency
     const size_t per_block = kLdsPerCu / static_cast<size_t>(std::max(per_cu, 1));
     const size_t fixed = static_cast<size_t>(scene_lds_words) * 4 + stack_bytes;
-    const size_t level_bytes = static_cast<size_t>(rt::kWavesPerBlock) * 3 * 64 * 4;
     if (per_block > fixed) {
       // keep 1 KiB per block in reserve: resident blocks whose LDS sums to within ~1% of 160 KiB were
       // measured NOT to be co-resident on gfx950 (3 x 53808 B: a third of the blocks started late)
-      const uint32_t fit = per_block > fixed + kLdsReserve ? static_cast<uint32_t>((per_block - fixed - kLdsReserve) / level_bytes) : 0u;
-      const uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
+      uint32_t fit = per_block > fixed + kLdsReserve ? static_cast<uint32_t>((per_block - fixed - kLdsReserve) / level_bytes) : 0u;
+      uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
+      if (narrow) lv = std::max<uint32_t>(lv & ~1u, rc_levels);   // even (rc_levels already is)
       if (lv > rc_levels) {
         const size_t lds2 = fixed + lv * level_bytes;
         int per_cu2 = jit_fn ? rt::jit_blocks_per_cu(jit_fn, lds2) : rt::render_blocks_per_cu(c->variant, lds2);
         if (c->blocks_per_cu > 0) per_cu2 = std::min(c->blocks_per_cu, per_cu2);
         if (per_cu2 >= per_cu) {
           rc_levels = lv;
-          rc_lds_words = rt::kWavesPerBlock * rc_levels * 3 * 64;
           c->lds_bytes = lds2;
         }
       }
     }
   }
+  const uint32_t rc_lds_words = static_cast<uint32_t>(rc_levels * level_bytes / 4);
   uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
                     static_cast<uint64_t>(c->cu_count);
   const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
@@ -475,15 +487,18 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     std::fprintf(stderr, "[rt] launch: traversal %d, %d blocks/CU, %llu blocks, lds %zu B (scene %u words, colour-stack levels %u, stack cap %u)\n",
                  trav, per_cu, static_cast<unsigned long long>(blocks), c->lds_bytes, scene_lds_words, rc_levels, stack_cap);
 
-  if (c->rng.ensure(static_cast<size_t>(n) * 6 * 4) != hipSuccess) return RT_ERR_HIP;
-  if (c->rc.ensure(static_cast<size_t>(mb) * 3 * threads * 4) != hipSuccess) return RT_ERR_HIP;
+  const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
+  const uint32_t n_ids = 64u * ((static_cast<uint32_t>(p->row_count) + 7) / 8) * tiles_x;
+  if (c->rng.ensure(static_cast<size_t>(n_ids) * 6 * 4) != hipSuccess) return RT_ERR_HIP;
+  if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;
 
   rt::SeedArgs sa{};
   sa.jump = static_cast<const uint32_t *>(c->jump.p);
   rt::xorwow_seed_base(p->seed, sa.base);
   sa.width = p->width; sa.row_offset = p->row_offset; sa.row_stride = p->row_stride;
-  sa.n_pixels = n;
-  sa.per_thread = c->seed_per_thread;
+  sa.rows = static_cast<uint32_t>(p->row_count);
+  sa.tiles_x = tiles_x;
+  sa.n_ids = n_ids;
   sa.rng = static_cast<uint32_t *>(c->rng.p);
 
   rt::RenderArgs a{};
@@ -500,6 +515,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
   a.rc_lds_word = scene_lds_words;
   a.rc_lds_levels = rc_levels;
+  a.rc_tex0 = c->img.mat_count;
+  a.rc_consts = c->img.rec_consts;
   a.stack_lds_word = scene_lds_words + rc_lds_words;
   const rtr_vec3 *v3s[6] = {&cam->pixel00, &cam->delta_u, &cam->delta_v, &cam->center, &cam->defocus_u, &cam->defocus_v};
   float *dst[6] = {a.p00, a.du, a.dv, a.center, a.dfu, a.dfv};
@@ -512,12 +529,12 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.sample_scale = 1.0f / static_cast<float>(p->samples_per_pixel);   // :1657
   a.n_pixels = n;
   a.rows = static_cast<uint32_t>(p->row_count);
-  a.tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
-  a.n_ids = 64u * ((a.rows + 7) / 8) * a.tiles_x;
+  a.tiles_x = tiles_x;
+  a.n_ids = n_ids;
   a.rng = static_cast<const uint32_t *>(c->rng.p);
   a.out = out_dev;
   a.out8 = out8_dev;
-  a.rc = static_cast<float *>(c->rc.p);
+  a.rc = c->rc.p;
   a.threads = threads;
   a.work = static_cast<uint32_t *>(c->work.p);
   a.counters = static_cast<unsigned long long *>(c->counters.p);
@@ -727,7 +744,8 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
   const uint32_t mb = static_cast<uint8_t>(max_bounces);
   const int variant = (img.words.size() <= rt::kLdsSceneMaxWords ? rt::kVarLds : 0) | (img.has_noise ? rt::kVarNoise : 0) |
                       (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img) |
-                      (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0);
+                      (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
+                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts <= 65536u ? rt::kVarNarrow : 0);
   std::string src;
   if (traversal == RT_TRAV_STATIC) {
     uint32_t v = 0;
@@ -758,10 +776,14 @@ int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int
   if (n > 0x7fffffffull) return RT_ERR_INVALID_ARG;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RT_ERR_NO_DEVICE;
+  const uint32_t tiles_x = (static_cast<uint32_t>(width) + 7) / 8;
+  const uint64_t n_ids = 64ull * ((static_cast<uint64_t>(rows) + 7) / 8) * tiles_x;
+  if (n_ids > 0xffffffffull) return RT_ERR_INVALID_ARG;
   const std::vector<uint32_t> &J = rt::xorwow_jump_tables();
   DevBuf jump, states;
+  std::vector<uint32_t> tiled;
   int rc = RT_OK;
-  if (jump.ensure(J.size() * 4) != hipSuccess || states.ensure(n * 6 * 4) != hipSuccess ||
+  if (jump.ensure(J.size() * 4) != hipSuccess || states.ensure(n_ids * 6 * 4) != hipSuccess ||
       hipMemcpy(jump.p, J.data(), J.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     rc = RT_ERR_HIP;
   } else {
@@ -769,16 +791,25 @@ int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int
     sa.jump = static_cast<const uint32_t *>(jump.p);
     rt::xorwow_seed_base(seed, sa.base);
     sa.width = width; sa.row_offset = row_offset; sa.row_stride = row_stride;
-    sa.n_pixels = static_cast<uint32_t>(n);
-    sa.per_thread = 16;
+    sa.rows = static_cast<uint32_t>(rows);
+    sa.tiles_x = tiles_x;
+    sa.n_ids = static_cast<uint32_t>(n_ids);
     sa.rng = static_cast<uint32_t *>(states.p);
+    tiled.resize(n_ids * 6);
     if (rt::launch_seed(sa, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(out, states.p, n * 6 * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(tiled.data(), states.p, n_ids * 6 * 4, hipMemcpyDeviceToHost) != hipSuccess)
       rc = RT_ERR_HIP;
   }
   jump.release();
   states.release();
-  return rc;
+  if (rc != RT_OK) return rc;
+  // tile-major (the kernels' layout) -> [6][rows * width] in pixel order (this function's contract)
+  for (uint64_t lr = 0; lr < static_cast<uint64_t>(rows); ++lr)
+    for (uint64_t j = 0; j < static_cast<uint64_t>(width); ++j) {
+      const uint64_t id = ((lr >> 3) * tiles_x + (j >> 3)) * 64 + (lr & 7) * 8 + (j & 7);
+      for (int w = 0; w < 6; ++w) out[w * n + lr * width + j] = tiled[w * n_ids + id];
+    }
+  return RT_OK;
 }
 
 const char *rt_context_note(const rt_context *c) { return c ? c->jit_why.c_str() : ""; }

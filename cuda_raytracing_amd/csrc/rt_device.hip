@@ -58,6 +58,10 @@ __device__ __forceinline__ void jump_next(const uint4 *__restrict__ lo, const ui
   x0 = r0; x1 = r1; x2 = r2; x3 = r3; x4 = r4;
 }
 
+// Thread t seeds a run of kSeedRun consecutive pixels of one row (one jump, then P_0 steps).  Threads
+// are ordered (8-row band, run, row in band): the 8 rows of a run are consecutive lanes, so each store
+// step of a wave fills whole 32-B row segments of 8x8 tiles in the tile-major state layout
+// (RenderArgs::rng) — the render then reads a tile's 64 states as 256 contiguous bytes per word.
 __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
   __shared__ uint4 s_lo[kJumpNibbles * 16];
   __shared__ uint32_t s_hi[kJumpNibbles * 16];
@@ -68,24 +72,26 @@ __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
     __syncthreads();
   }
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-  const uint64_t l0 = static_cast<uint64_t>(t) * A.per_thread;
-  if (l0 >= A.n_pixels) return;
-  const uint32_t l1 = static_cast<uint32_t>(min<uint64_t>(l0 + A.per_thread, A.n_pixels));
-  uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0;
-  const uint32_t n = A.n_pixels;
-  for (uint32_t l = static_cast<uint32_t>(l0); l < l1; ++l) {
-    const uint32_t lr = l / A.width, j = l - lr * A.width;
-    if (l == l0 || j == 0) {
-      const uint64_t g = static_cast<uint64_t>(A.row_offset + static_cast<int64_t>(lr) * A.row_stride) * A.width + j;
-      x0 = A.base[1]; x1 = A.base[2]; x2 = A.base[3]; x3 = A.base[4]; x4 = A.base[5];
-      if (g & 1u) jump_next(s_lo, s_hi, x0, x1, x2, x3, x4);
-      for (int k = 1; k < kJumpPowers; ++k)
-        if ((g >> k) & 1u) jump_apply(A.jump + k * kJumpMatrixWords, x0, x1, x2, x3, x4);
-    } else {
-      jump_next(s_lo, s_hi, x0, x1, x2, x3, x4);     // P_0: next global pixel in the row
-    }
-    A.rng[l] = A.base[0];
-    A.rng[n + l] = x0; A.rng[2 * n + l] = x1; A.rng[3 * n + l] = x2; A.rng[4 * n + l] = x3; A.rng[5 * n + l] = x4;
+  const uint32_t W = static_cast<uint32_t>(A.width);
+  const uint32_t runs = (W + kSeedRun - 1) / kSeedRun;
+  const uint32_t band = t / (8u * runs), q = t - band * 8u * runs;
+  const uint32_t lr = band * 8u + (q & 7u), j0 = (q >> 3) * kSeedRun;
+  if (lr >= A.rows) return;
+  const uint32_t j1 = min(j0 + kSeedRun, W);
+  uint32_t x0 = A.base[1], x1 = A.base[2], x2 = A.base[3], x3 = A.base[4], x4 = A.base[5];
+  {
+    const uint64_t g = static_cast<uint64_t>(A.row_offset + static_cast<int64_t>(lr) * A.row_stride) * W + j0;
+    if (g & 1u) jump_next(s_lo, s_hi, x0, x1, x2, x3, x4);
+    for (int k = 1; k < kJumpPowers; ++k)
+      if ((g >> k) & 1u) jump_apply(A.jump + k * kJumpMatrixWords, x0, x1, x2, x3, x4);
+  }
+  const uint32_t n = A.n_ids;
+  const uint32_t row_base = (lr >> 3) * A.tiles_x * 64u + (lr & 7u) * 8u;
+  for (uint32_t j = j0; j < j1; ++j) {
+    if (j > j0) jump_next(s_lo, s_hi, x0, x1, x2, x3, x4);     // P_0: next global pixel in the row
+    const uint32_t id = row_base + (j >> 3) * 64u + (j & 7u);
+    A.rng[id] = A.base[0];
+    A.rng[n + id] = x0; A.rng[2 * n + id] = x1; A.rng[3 * n + id] = x2; A.rng[4 * n + id] = x3; A.rng[5 * n + id] = x4;
   }
 }
 
@@ -154,7 +160,8 @@ hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipSt
 }
 
 hipError_t launch_seed(const SeedArgs &a, hipStream_t s) {
-  const uint64_t threads = (static_cast<uint64_t>(a.n_pixels) + a.per_thread - 1) / a.per_thread;
+  const uint64_t runs = (static_cast<uint64_t>(a.width) + kSeedRun - 1) / kSeedRun;
+  const uint64_t threads = (static_cast<uint64_t>(a.rows) + 7) / 8 * 8 * runs;
   const uint32_t blocks = static_cast<uint32_t>((threads + kBlock - 1) / kBlock);
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(seed_kernel, dim3(blocks), dim3(kBlock), 0, s, a);

@@ -71,7 +71,7 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
                 bool *folded) {
   std::string trace;
   if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
-  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | (15 << kVarMatShift) | (15 << kVarTexShift));
+  const int v = variant & kJitVarMask;
   // RT_JIT_WAVES=N asks the register allocator for N waves per SIMD (A/B; default: unconstrained)
   std::string attr;
   if (const char *e = std::getenv("RT_JIT_WAVES"))
@@ -300,7 +300,7 @@ uint32_t scene_kinds(const SceneImage &img) {
 }
 
 std::string jit_lane_source(const SceneImage &img, int variant) {
-  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | (15 << kVarMatShift) | (15 << kVarTexShift));
+  const int v = variant & kJitVarMask;
   const std::string lt = "LaneTraceK<" + std::to_string(scene_kinds(img)) + "u, true>";   // pausable walk
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render(RenderArgs A) {\n  render_body<" +
@@ -314,7 +314,7 @@ std::string jit_lane_source(const SceneImage &img, int variant) {
 }
 
 std::string jit_accel_source(const SceneImage &img, int variant) {
-  const int v = variant & (kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | (15 << kVarMatShift) | (15 << kVarTexShift));
+  const int v = variant & kJitVarMask;
   const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u>";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render(RenderArgs A) {\n  render_body<" +

@@ -320,6 +320,17 @@ int compile_scene(const void *scene_ptr, SceneImage *img) {
   W.insert(W.end(), c.mats.begin(), c.mats.end());
   img->off_texs = static_cast<uint32_t>(W.size());
   W.insert(W.end(), c.texs.begin(), c.texs.end());
+  // constant colour records (rt_layout.h kRcConsts): magenta, black, NaN grey at words 1..3
+  img->rec_consts = img->mat_count + img->tex_count;
+  {
+    const float nan = std::nanf("");
+    const float rgb[kRcConsts][3] = {{1.0f, 0.0f, 1.0f}, {0.0f, 0.0f, 0.0f}, {nan, nan, nan}};
+    for (uint32_t k = 0; k < kRcConsts; ++k) {
+      uint32_t w[kRecWords] = {0xffffffffu};
+      for (int ch = 0; ch < 3; ++ch) w[1 + ch] = fbits(rgb[k][ch]);
+      W.insert(W.end(), w, w + kRecWords);
+    }
+  }
   while (W.size() % 4) W.push_back(0);   // float4 alignment for the gradient table
   img->off_perlin = static_cast<uint32_t>(W.size());
   W.insert(W.end(), c.perlin.begin(), c.perlin.end());
