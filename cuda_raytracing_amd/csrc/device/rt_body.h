@@ -739,34 +739,47 @@ using LaneTrace = LaneTraceK<0x7fu>;
 // The box arrives padded by the subtree's share kAccelKappa * M; the ray's share kAccelKappa * |o|_1
 // is added in t (pinv = that pad * |1/d| per axis).  Slab values by fma with oinv = o * (1/d): this
 // test only has to be conservative, and its rounding (~u |o| in space) is far inside the padding.
-__device__ __forceinline__ bool accel_box(const Trav &T, f3 oinv, f3 pinv, float x0, float x1, float y0, float y1,
+// Per ray: which slab plane is the near one on each axis (sign of 1/d) and the t offsets with the ray's
+// padding share folded in: near t = fma(x_near, 1/d, on), far t = fma(x_far, 1/d, of), on/of =
+// -o/d -+ pad |1/d| (one more rounding of ~u |o/d|, again far inside the padding).
+struct SlabRay {
+  f3 on, of;
+  bool nx, ny, nz;   // 1/d < 0: the near plane is the box's max
+};
+__device__ __forceinline__ SlabRay slab_ray(const Trav &T, f3 oinv, f3 pinv) {
+  SlabRay s;
+  s.on = mk(-oinv.x - pinv.x, -oinv.y - pinv.y, -oinv.z - pinv.z);
+  s.of = mk(-oinv.x + pinv.x, -oinv.y + pinv.y, -oinv.z + pinv.z);
+  s.nx = T.inv.x < 0.0f; s.ny = T.inv.y < 0.0f; s.nz = T.inv.z < 0.0f;
+  return s;
+}
+__device__ __forceinline__ bool accel_box(const Trav &T, const SlabRay &R, float x0, float x1, float y0, float y1,
                                           float z0, float z1, float *tnear) {
-  float a = __builtin_fmaf(x0, T.inv.x, -oinv.x), c = __builtin_fmaf(x1, T.inv.x, -oinv.x);
-  float t0 = fmaxf(kTmin, fminf(a, c) - pinv.x), t1 = fminf(T.tmax, fmaxf(a, c) + pinv.x);
-  a = __builtin_fmaf(y0, T.inv.y, -oinv.y); c = __builtin_fmaf(y1, T.inv.y, -oinv.y);
-  t0 = fmaxf(t0, fminf(a, c) - pinv.y); t1 = fminf(t1, fmaxf(a, c) + pinv.y);
-  a = __builtin_fmaf(z0, T.inv.z, -oinv.z); c = __builtin_fmaf(z1, T.inv.z, -oinv.z);
-  t0 = fmaxf(t0, fminf(a, c) - pinv.z); t1 = fminf(t1, fmaxf(a, c) + pinv.z);
+  const float nx = __builtin_fmaf(R.nx ? x1 : x0, T.inv.x, R.on.x), fx = __builtin_fmaf(R.nx ? x0 : x1, T.inv.x, R.of.x);
+  const float ny = __builtin_fmaf(R.ny ? y1 : y0, T.inv.y, R.on.y), fy = __builtin_fmaf(R.ny ? y0 : y1, T.inv.y, R.of.y);
+  const float nz = __builtin_fmaf(R.nz ? z1 : z0, T.inv.z, R.on.z), fz = __builtin_fmaf(R.nz ? z0 : z1, T.inv.z, R.of.z);
+  const float t0 = fmaxf(fmaxf(nx, ny), fmaxf(nz, kTmin)), t1 = fminf(fminf(fx, fy), fminf(fz, T.tmax));
   *tnear = t0;
   return !(t1 < t0);
 }
 
-// sphere branch of hit() with the record commit of sphere_hit<UV>; also reports a root equal to tmax
+// sphere branch of hit() with the record commit of sphere_hit<UV>; also reports a root equal to tmax.
+// a = dot(d, d), 4 * a and 2 * a are the same for every sphere of the walk (the ray is not transformed
+// in an all-sphere world): computed once per ray by the caller, the same IEEE operations.
 template <bool UV>
 __device__ __forceinline__ bool sphere_hit_tie(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
-                                               float inv_rad, bool &tie) {
+                                               float inv_rad, float a4, float a2, bool &tie) {
   f3 center = line_at(c0, r.time, mv);
   f3 oc = sub(center, r.o);
-  float a = dot(r.d, r.d);
   float b = -2.0f * dot(r.d, oc);
   float c = dot(oc, oc) - rad2;
-  float disc = b * b - 4 * a * c;
+  float disc = b * b - a4 * c;
   if (!(disc >= 0)) return false;
   float sq = sqrtf(disc);
-  float root = (-b - sq) / (2.0f * a);
+  float root = (-b - sq) / a2;
   tie |= root == T.tmax;
   if (kTmin >= root || root >= T.tmax) {
-    root = (-b + sq) / (2.0f * a);
+    root = (-b + sq) / a2;
     tie |= root == T.tmax;
   }
   if (!(kTmin < root && root < T.tmax)) return false;
@@ -811,12 +824,14 @@ struct AccelTraceK {
       const float pad_o = kAccelKappa * ao;
       const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
       const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
+      const SlabRay sr = slab_ray(T, oinv, pinv);
+      const float sa = dot(r.d, r.d), sa4 = 4 * sa, sa2 = 2.0f * sa;   // sphere_hit_tie's per-ray terms
       auto leaf = [&](uint32_t ref) {
         const uint32_t first = ref & 0xffffffu, cnt = ((ref >> 24) & 0x7fu) + 1u;
         for (uint32_t k = 0; k < cnt; ++k) {
           const uint4 p0 = P[(first + k) * 4], p1 = P[(first + k) * 4 + 1], p2 = P[(first + k) * 4 + 2];
           if (sphere_hit_tie<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
-                                 asf(p1.z), asf(p1.w), tie))
+                                 asf(p1.z), asf(p1.w), sa4, sa2, tie))
             best = first + k;
         }
       };
@@ -832,8 +847,8 @@ struct AccelTraceK {
         if (walking) {
         const uint4 q0 = N[node * 4], q1 = N[node * 4 + 1], q2 = N[node * 4 + 2], q3 = N[node * 4 + 3];
         float n0, n1;
-        bool h0 = accel_box(T, oinv, pinv, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), &n0);
-        bool h1 = accel_box(T, oinv, pinv, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w), &n1);
+        bool h0 = accel_box(T, sr, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), &n0);
+        bool h1 = accel_box(T, sr, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w), &n1);
         const bool near0 = n0 <= n1;
         const uint32_t rn = near0 ? q3.x : q3.y, rf = near0 ? q3.y : q3.x;
         bool hn = near0 ? h0 : h1, hf = near0 ? h1 : h0;
