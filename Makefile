@@ -22,7 +22,7 @@ HIP_FLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno
               -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-rdc -fno-slp-vectorize -Wall
 ORACLE_FLAGS := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -fopenmp -Wall -Wextra
 
-HOST_SRC := $(CSRC)/host/rt_host.cpp
+HOST_SRC := $(CSRC)/host/rt_host.cpp $(CSRC)/host/image_load.cpp
 HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp \
             $(CSRC)/sphere_accel.cpp \
             $(CSRC)/scene_codegen.cpp $(CSRC)/rt_jit.cpp

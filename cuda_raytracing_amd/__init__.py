@@ -24,7 +24,7 @@ __all__ = [
     "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE",
     "RT_FLAG_NO_JIT", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_FLAG_FORCE_ACCEL", "RT_FLAG_NO_ACCEL", "RT_TRAV_ACCEL", "RT_TRAV_LANE",
     "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "accel_build", "tonemap_device", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
-    "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError",
+    "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError", "load_image",
 ]
 
 
@@ -84,7 +84,12 @@ class World:
         return self._L.rt_mat_lambert_checker(self._w, scale, vec3(*even), vec3(*odd))
 
     def image(self, name: str = "earthmap.jpg") -> _abi.Material:
+        """Image texture from a file (stbi_loadf semantics, load_image); a missing file renders magenta
+        like the reference's failed load, an undecodable one makes status() RT_ERR_UNSUPPORTED."""
         return self._L.rt_mat_lambert_image(self._w, name.encode())
+
+    def status(self) -> int:
+        return int(self._L.rt_world_status(self._w))
 
     def image_pixels(self, rgb) -> _abi.Material:
         """Image texture with texels (float32 [H, W, 3], like stbi_loadf) — copied into the arena."""
@@ -203,6 +208,23 @@ def build_scene(index: int, capacity: int | None = None):
     s = w.build_scene(index)
     w.build_bvh()
     return w, s
+
+
+def load_image(path: str):
+    """rt_image_load: float32 [H, W, 3] texels (row 0 = top, 8-bit channels as powf(c/255, 2.2)), or None
+    when the file does not exist (the reference's failed load).  RenderError(RT_ERR_UNSUPPORTED) for a
+    format other than binary PNM / BMP / TGA."""
+    L = _abi.host_lib()
+    p = C.POINTER(C.c_float)()
+    w, h = C.c_int32(0), C.c_int32(0)
+    rc = L.rt_image_load(str(path).encode(), C.byref(p), C.byref(w), C.byref(h))
+    if rc == 1:   # RT_IMAGE_MISSING
+        return None
+    _check(rc, f"load image {path}")
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
+    finally:
+        L.rt_image_free(p)
 
 
 def camera_from_settings(settings: Settings, width: int = 0, height: int = 0):

@@ -144,6 +144,10 @@ def host_lib():
             _sig(getattr(L, name), Material, P, Vec3)
         _sig(L.rt_mat_lambert_image, Material, P, C.c_char_p)
         _sig(L.rt_mat_lambert_image_pixels, Material, P, P, C.c_int32, C.c_int32)
+        _sig(L.rt_world_status, C.c_int, P)
+        _sig(L.rt_image_load, C.c_int, C.c_char_p, C.POINTER(C.POINTER(C.c_float)), C.POINTER(C.c_int32),
+             C.POINTER(C.c_int32))
+        _sig(L.rt_image_free, None, C.POINTER(C.c_float))
         _sig(L.rt_mat_lambert_noise, Material, P, C.c_float)
         _sig(L.rt_mat_metal, Material, Vec3, C.c_float)
         _sig(L.rt_mat_dielectric, Material, C.c_float)

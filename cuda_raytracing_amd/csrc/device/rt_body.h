@@ -17,6 +17,9 @@
 #ifndef RT_UNWIND_LDS
 #define RT_UNWIND_LDS 3     // LDS colour-stack levels loaded per batch in the unwind
 #endif
+#ifndef RT_UNWIND_LDS_DEEP
+#define RT_UNWIND_LDS_DEEP 8   // ... in deep-path kernels (max_bounces > kDeepBounces)
+#endif
 
 namespace rt {
 
@@ -398,6 +401,25 @@ __device__ __forceinline__ f3 rc_decode(const Mem<LDS> &S, const RenderArgs &A, 
   const uint32_t o = grey ? A.off_mats : (texel ? A.off_pixels + (w & kRcPayload) : A.off_mats + (w & kRcPayload) * kRecWords + 1);
   const f3 c = mk(S.f(o), S.f(o + 1), S.f(o + 2));
   return grey ? mk(asf(w), asf(w), asf(w)) : c;
+}
+
+// a batch of codes: in kernels with noise textures the record loads are skipped when every code of the
+// batch is a grey in every lane (wave-uniform test) — a deep path between noise surfaces is all greys
+template <bool LDS, bool WIDE, bool NOISE, bool UV, int N>
+__device__ __forceinline__ void rc_decode_batch(const Mem<LDS> &S, const RenderArgs &A, const uint32_t (&cw)[N],
+                                                f3 (&at)[N]) {
+  if (NOISE) {
+    bool rec = false;
+#pragma unroll
+    for (int i = 0; i < N; ++i) rec |= (cw[i] & kRcRecTag) == kRcRecTag;
+    if (__ballot(rec) == 0) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) at[i] = mk(asf(cw[i]), asf(cw[i]), asf(cw[i]));
+      return;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) at[i] = rc_decode<LDS, WIDE, NOISE, UV>(S, A, cw[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1364,26 +1386,25 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 #pragma unroll
         for (int i = 0; i < kUnwindBatch; ++i) cw[i] = rc_hbm_load(static_cast<uint32_t>(max(k - i, kl)));
         f3 at[kUnwindBatch];
-#pragma unroll
-        for (int i = 0; i < kUnwindBatch; ++i) at[i] = rc_decode<LDS, WIDE, NOISE, UV>(S, A, cw[i]);
+        rc_decode_batch<LDS, WIDE, NOISE, UV>(S, A, cw, at);
 #pragma unroll
         for (int i = 0; i < kUnwindBatch; ++i)
           if (k - i >= kl) res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
         k -= kUnwindBatch;
         if (k < kl) k = kl - 1;   // continue with the deepest LDS level
       }
-      // LDS levels, RT_UNWIND_LDS at a time: the code loads of a batch are issued together, then their
+      // LDS levels, kLdsBatch at a time: the code loads of a batch are issued together, then their
       // decodes (one LDS latency each per batch, not per level).  Levels below 0 read level 0 and
       // multiply by 1.0f instead (exact).
-      for (; k >= 0; k -= RT_UNWIND_LDS) {
-        uint32_t cw[RT_UNWIND_LDS];
+      constexpr int kLdsBatch = DEEP ? RT_UNWIND_LDS_DEEP : RT_UNWIND_LDS;
+      for (; k >= 0; k -= kLdsBatch) {
+        uint32_t cw[kLdsBatch];
 #pragma unroll
-        for (int i = 0; i < RT_UNWIND_LDS; ++i) cw[i] = rc_lds_load(static_cast<uint32_t>(max(k - i, 0)));
-        f3 at[RT_UNWIND_LDS];
+        for (int i = 0; i < kLdsBatch; ++i) cw[i] = rc_lds_load(static_cast<uint32_t>(max(k - i, 0)));
+        f3 at[kLdsBatch];
+        rc_decode_batch<LDS, WIDE, NOISE, UV>(S, A, cw, at);
 #pragma unroll
-        for (int i = 0; i < RT_UNWIND_LDS; ++i) at[i] = rc_decode<LDS, WIDE, NOISE, UV>(S, A, cw[i]);
-#pragma unroll
-        for (int i = 0; i < RT_UNWIND_LDS; ++i) {
+        for (int i = 0; i < kLdsBatch; ++i) {
           if (k - i < 0) at[i] = mk(1.0f, 1.0f, 1.0f);
           res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
         }

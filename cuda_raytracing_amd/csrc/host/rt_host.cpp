@@ -169,6 +169,7 @@ struct rt_world {
   uint64_t arena_cap;
   rt::GlibcRand rng;
   bool failed = false;
+  bool unsupported = false;   // an image file exists in a format this build does not decode
 
   // utility.h:26-41
   float random_f32() { return static_cast<float>(rng.next()) / (2147483647 + 1.0f); }
@@ -437,14 +438,26 @@ rtr_material rt_mat_light_solid(rt_world *w, rtr_vec3 color) {
   return mat_with_tex(RTR_MAT_DIFFUSE_LIGHT, w->solid_texture(color));
 }
 rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name) {
-  // raytracing.cu:332-341 via stb_image.  The reference's only image (earthmap.jpg) is not in its
-  // repository, so stbi_loadf fails: pixels == NULL, width = height = 0 and the texture renders
-  // magenta (raytracing.cu:346-347).  Image decoding is out of scope; a failed load is
-  // what every reference run sees.
-  (void)file_name;
+  // raytracing.cu:332-341 via stbi_loadf (image_load.cpp).  A missing file is the reference's failed
+  // load: pixels == NULL, width = height = 0, the texture renders magenta (:346-347) — the catalog's
+  // earthmap.jpg is not in the reference repository, so that is what every reference run sees.  A file
+  // in a format this build does not decode makes the world RT_ERR_UNSUPPORTED (rt_world_status).
+  float *rgb = nullptr;
+  int32_t width = 0, height = 0;
+  const int st = rt_image_load(file_name, &rgb, &width, &height);
+  if (st == RT_OK) {
+    rtr_material m = rt_mat_lambert_image_pixels(w, rgb, width, height);
+    rt_image_free(rgb);
+    return m;
+  }
+  if (st != RT_IMAGE_MISSING) w->unsupported = true;
   rtr_texture t; std::memset(&t, 0, sizeof t);
   t.kind = RTR_TEX_IMAGE;
   return mat_with_tex(RTR_MAT_LAMBERTIAN, w->texture_add(t, nullptr, nullptr, 0));
+}
+int rt_world_status(const rt_world *w) {
+  if (!w) return RT_ERR_INVALID_ARG;
+  return w->failed ? RT_ERR_SCENE : (w->unsupported ? RT_ERR_UNSUPPORTED : RT_OK);
 }
 rtr_material rt_mat_lambert_image_pixels(rt_world *w, const float *rgb, int32_t width, int32_t height) {
   // what make_image_texture (:332-341) builds when stbi_loadf succeeds: float RGB texels copied into
@@ -796,7 +809,7 @@ int rt_world_build_scene(rt_world *w, int index, rt_settings *s) {
       break;
     default: return RT_ERR_INVALID_ARG;
   }
-  return w->failed ? RT_ERR_SCENE : RT_OK;
+  return rt_world_status(w);
 }
 
 // ---- camera (raytracing.cu:1657-1692) ----

@@ -55,13 +55,18 @@ int rt_world_scene(const rt_world *w, uint16_t root, rt_scene *out);
 uint32_t rt_world_hittable_count(const rt_world *w);
 uint32_t rt_world_ref_count(const rt_world *w);
 uint64_t rt_world_texture_bytes(const rt_world *w);
+/* RT_OK, RT_ERR_SCENE (capacity or arena exhausted) or RT_ERR_UNSUPPORTED (undecodable image file) */
+int rt_world_status(const rt_world *w);
 /* raw glibc rand() from the world's stream (tests) */
 int32_t rt_world_rand(rt_world *w);
 
 /* ---- scene builder API (raytracing.cu:1775-1977); materials are returned by value ---- */
 rtr_material rt_mat_lambert_solid(rt_world *w, rtr_vec3 albedo);                 /* :1805 */
 rtr_material rt_mat_light_solid(rt_world *w, rtr_vec3 color);                    /* :1813 */
-rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name);           /* :1821 */
+/* :1821.  Loads the file like stbi_loadf(file, .., 3) (image_load.cpp: binary PNM, BMP, TGA).  A missing
+ * file is the reference's failed load (magenta texture); an existing file in another format sets the
+ * world's status to RT_ERR_UNSUPPORTED (rt_world_status, returned by rt_world_build_scene). */
+rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name);
 /* an image texture whose load succeeded: width*height float RGB texels (stbi_loadf layout, row 0 first) */
 rtr_material rt_mat_lambert_image_pixels(rt_world *w, const float *rgb, int32_t width, int32_t height);
 rtr_material rt_mat_lambert_noise(rt_world *w, float scale);                     /* :1829 */
@@ -83,6 +88,14 @@ int rt_add_box(rt_world *w, int xf, float angle, rtr_vec3 offset,
                rtr_vec3 a, rtr_vec3 b, rtr_material mat);
 int rt_add_pyramid(rt_world *w, int xf, float angle, rtr_vec3 offset,
                    rtr_vec3 base_a, rtr_vec3 base_b, rtr_vec3 tip, rtr_material mat);
+
+/* ---- image files (make_image_texture's stbi_loadf, raytracing.cu:332-341) ----
+ * *rgb = width*height float RGB texels, row 0 = top, 8-bit channels as powf(c/255, 2.2) (stb_image's
+ * LDR->float rule); free with rt_image_free.  Returns RT_OK, RT_IMAGE_MISSING (no such file: the
+ * reference's failed load) or RT_ERR_UNSUPPORTED (a format other than binary PNM / BMP / TGA). */
+#define RT_IMAGE_MISSING 1
+int rt_image_load(const char *path, float **rgb, int32_t *width, int32_t *height);
+void rt_image_free(float *rgb);
 
 /* ---- camera (raytracing.cu:1657-1692).  width/height <= 0 => reference rule
  * W = settings.img_width, H = (int)(W / img_ratio) (:1659-1660). ---- */

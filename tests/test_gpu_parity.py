@@ -314,6 +314,32 @@ def test_image_texture_scene_vs_oracle():
         assert np.array_equal(bits(fb), bits(ref)), force
 
 
+def test_earth_scene_with_a_texture_file_vs_oracle(tmp_path, monkeypatch):
+    # the catalog's earth scene (raytracing.cu:2042-2052) with an earthmap file this build decodes (a
+    # 24-bit BMP written here; the reference's JPEG is absent): texels loaded like stbi_loadf, rendered
+    # on the GPU and by the oracle from the same arena bytes
+    import struct
+    rng = np.random.default_rng(3)
+    h, w_ = 32, 64
+    pic = rng.integers(0, 256, size=(h, w_, 3), dtype=np.uint8)
+    stride = (w_ * 3 + 3) & ~3
+    rows = b"".join(pic[y, :, ::-1].tobytes() + b"\0" * (stride - 3 * w_) for y in range(h - 1, -1, -1))
+    bmp = struct.pack("<2sIHHI", b"BM", 54 + len(rows), 0, 0, 54) + \
+        struct.pack("<IiiHHIIiiII", 40, w_, h, 1, 24, 0, len(rows), 0, 0, 0, 0) + rows
+    (tmp_path / "earthmap.jpg").write_bytes(bmp)   # the scene's file name; the loader reads the BMP magic
+    monkeypatch.chdir(tmp_path)
+    idx = [rt.scene_name(i) for i in range(rt.RT_SCENE_COUNT)].index("earth")
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 128, 72)
+    p = rt.make_params(s, W, H, spp=2, bounces=6)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    px = ref.reshape(-1, 3)
+    assert rc == 0 and len(np.unique(px, axis=0)) > 100   # textured
+    assert not np.any((px[:, 0] > 0) & (px[:, 1] == 0) & (px[:, 2] > 0))   # no magenta (failed-load) texel
+    fb, st = gpu(w.scene(), cam, p)
+    assert np.array_equal(bits(fb), bits(ref))
+
+
 @pytest.mark.parametrize("idx,W,H,spp", [(2, 64, 36, 4), (20, 64, 36, 4), (20, 160, 90, 6), (2, 128, 72, 8)])
 def test_verified_sphere_traversal_matches_oracle(idx, W, H, spp):
     # SAH tree walk + per-ray proof against the reference tree (fallback to the reference walk)
