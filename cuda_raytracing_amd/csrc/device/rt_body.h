@@ -1103,6 +1103,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 
   uint32_t chunk_pos = 0, chunk_end = 0;   // wave-uniform: ids of the wave's current tile
   bool exhausted = false;
+  bool prio_done = false;                  // wave-uniform: the split costliest tiles are all handed out
   uint32_t tiles_taken = 0, rounds = 0;
   uint32_t probe_tile = 0, probe_rounds = 0;
   uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, ph_unwind = 0, ph_cam = 0, t_mark = 0;   // wave-trace clocks
@@ -1156,14 +1157,24 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     uint64_t m = __ballot(need);
     while (m != 0 && !exhausted) {
       if (chunk_pos >= chunk_end) {
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(A.work, static_cast<uint32_t>(kChunk));
+        // the costliest tiles (the first prio_ids ids of the longest-first order) may be handed out in
+        // prio_chunk-pixel pieces from their own counter, so that their long pixel chains spread over
+        // more waves; every other tile goes out whole
+        uint32_t base = 0, size = static_cast<uint32_t>(kChunk);
+        const bool split = A.prio_chunk < static_cast<uint32_t>(kChunk) && !prio_done;
+        if (lane == 0) {
+          if (split) base = atomicAdd(A.work + 1, A.prio_chunk);
+          if (!split || base >= A.prio_ids) base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
+          else size = A.prio_chunk;
+        }
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
+        size = __builtin_amdgcn_readfirstlane(__shfl(size, 0));
+        if (size == static_cast<uint32_t>(kChunk)) prio_done = true;
         if (base >= A.n_ids) { exhausted = true; break; }
         if (A.reverse_tiles) base = A.n_ids - kChunk - base;   // whole tiles: n_ids is a multiple of 64
         tiles_taken++;
         chunk_pos = base;
-        chunk_end = min(base + static_cast<uint32_t>(kChunk), A.n_ids);
+        chunk_end = min(base + size, A.n_ids);
       }
       const uint32_t avail = chunk_end - chunk_pos;
       const uint32_t rank = __popcll(m & lt_mask);

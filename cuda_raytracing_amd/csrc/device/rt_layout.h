@@ -160,6 +160,7 @@ struct RenderArgs {
   uint32_t trace_min_iters;       // lanes (and <= 1/4 of the starters) still walk, after this many steps
   uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of
                                   // the longest-first order) run their wave at raised issue priority
+  uint32_t prio_chunk;            // < 64: those ids are handed out in pieces of this many (work[1])
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the
                                   // wave still need a try (they resume next round; 0 = never early)
   uint32_t black_skip;            // every attenuation is finite (host-checked): a path ending in
