@@ -848,15 +848,6 @@ struct AccelTraceK {
       const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
       const SlabRay sr = slab_ray(T, oinv, pinv);
       const float sa = dot(r.d, r.d), sa4 = 4 * sa, sa2 = 2.0f * sa;   // sphere_hit_tie's per-ray terms
-      auto leaf = [&](uint32_t ref) {
-        const uint32_t first = ref & 0xffffffu, cnt = ((ref >> 24) & 0x7fu) + 1u;
-        for (uint32_t k = 0; k < cnt; ++k) {
-          const uint4 p0 = P[(first + k) * 4], p1 = P[(first + k) * 4 + 1], p2 = P[(first + k) * 4 + 2];
-          if (sphere_hit_tie<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
-                                 asf(p1.z), asf(p1.w), sa4, sa2, tie))
-            best = first + k;
-        }
-      };
       uint32_t node = resume ? T.anode : A.accel_root;
       int sp = resume ? T.asp : 0;
       // Wave-uniform loop, one node per walking lane per step.  Rays differ wildly in length (the
@@ -874,8 +865,20 @@ struct AccelTraceK {
         const bool near0 = n0 <= n1;
         const uint32_t rn = near0 ? q3.x : q3.y, rf = near0 ? q3.y : q3.x;
         bool hn = near0 ? h0 : h1, hf = near0 ? h1 : h0;
-        if (hn && (rn & kAccelLeaf)) { leaf(rn); hn = false; }
-        if (hf && (rf & kAccelLeaf)) { leaf(rf); hf = false; }
+        // the hit leaves' spheres, near leaf first, in ONE per-lane loop (the wave runs the longest
+        // lane's count once, not the near and the far leaf's maxima one after the other)
+        const bool ln = hn && (rn & kAccelLeaf), lf = hf && (rf & kAccelLeaf);
+        const uint32_t c1 = ln ? ((rn >> 24) & 0x7fu) + 1u : 0u, c2 = lf ? ((rf >> 24) & 0x7fu) + 1u : 0u;
+        const uint32_t f1 = rn & 0xffffffu, f2 = (rf & 0xffffffu) - c1;
+        for (uint32_t k = 0; k < c1 + c2; ++k) {
+          const uint32_t pr = (k < c1 ? f1 : f2) + k;
+          const uint4 p0 = P[pr * 4], p1 = P[pr * 4 + 1], p2 = P[pr * 4 + 2];
+          if (sphere_hit_tie<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
+                                 asf(p1.z), asf(p1.w), sa4, sa2, tie))
+            best = pr;
+        }
+        hn = hn && !ln;
+        hf = hf && !lf;
         if (hn && hf) {
           stk[sp * 64] = static_cast<uint16_t>(rf);
           ++sp;
