@@ -67,6 +67,10 @@ struct Mem {
     return LDS ? reinterpret_cast<const uint8_t *>(&g_lds[word_base])[b]
                : reinterpret_cast<const uint8_t *>(&g[word_base])[b];
   }
+  __device__ __forceinline__ uint32_t half(uint32_t word_base, uint32_t k) const {
+    return LDS ? reinterpret_cast<const uint16_t *>(&g_lds[word_base])[k]
+               : reinterpret_cast<const uint16_t *>(&g[word_base])[k];
+  }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -229,10 +233,12 @@ __device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
   float fx = floorf(p.x), fy = floorf(p.y), fz = floorf(p.z);
   float u = p.x - fx, v = p.y - fy, w = p.z - fz;
   int32_t i = static_cast<int32_t>(fx), j = static_cast<int32_t>(fy), k = static_cast<int32_t>(fz);
-  const uint32_t pb = tb + 1024;   // perm_x bytes
-  uint32_t pi0 = S.byte(pb, i & 255), pi1 = S.byte(pb, (i + 1) & 255);
-  uint32_t pj0 = S.byte(pb, j & 255), pj1 = S.byte(pb, (j + 1) & 255);
-  uint32_t pk0 = S.byte(pb, k & 255), pk1 = S.byte(pb, (k + 1) & 255);
+  // perm_x[i & 255] and perm_x[(i + 1) & 255] from one u16 of the pair table
+  const uint32_t pb = tb + kPerlinPerm2Word;
+  const uint32_t qi = S.half(pb, i & 255), qj = S.half(pb, j & 255), qk = S.half(pb, k & 255);
+  uint32_t pi0 = qi & 255u, pi1 = qi >> 8;
+  uint32_t pj0 = qj & 255u, pj1 = qj >> 8;
+  uint32_t pk0 = qk & 255u, pk1 = qk >> 8;
   float uu = u * u * (3 - 2 * u);
   float vv = v * v * (3 - 2 * v);
   float ww = w * w * (3 - 2 * w);
@@ -240,6 +246,10 @@ __device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
   float wu[2] = {1 - uu, uu}, wv[2] = {1 - vv, vv}, wwk[2] = {1 - ww, ww};
   float du[2] = {u, u - 1.0f}, dv[2] = {v, v - 1.0f}, dw[2] = {w, w - 1.0f};
   uint32_t pi[2] = {pi0, pi1}, pj[2] = {pj0, pj1}, pk[2] = {pk0, pk1};
+  // the eight gradient gathers are issued before the arithmetic
+  uint4 gr[8];
+#pragma unroll
+  for (int c8 = 0; c8 < 8; ++c8) gr[c8] = S.w4(tb + 4 * ((pi[c8 >> 2] ^ pj[(c8 >> 1) & 1] ^ pk[c8 & 1]) & 255));
   float accum = 0.0f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -247,9 +257,8 @@ __device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        uint32_t g = (pi[a] ^ pj[b] ^ pk[c]) & 255;
-        uint4 gr = S.w4(tb + 4 * g);
-        f3 grad = mk(asf(gr.x), asf(gr.y), asf(gr.z));
+        const uint4 g = gr[4 * a + 2 * b + c];
+        f3 grad = mk(asf(g.x), asf(g.y), asf(g.z));
         accum += wu[a] * wv[b] * wwk[c] * dot(grad, mk(du[a], dv[b], dw[c]));
       }
   return accum;

@@ -71,8 +71,9 @@ enum : int {
 };
 
 // Perlin table: 256 gradients as float4 (xyz, pad) + 256 perm_x bytes (perm_y/z are never read,
-// perlin_noise.cpp:37-39)
-constexpr int kPerlinWords = 256 * 4 + 64;
+// perlin_noise.cpp:37-39) + 256 u16 pairs perm_x[i] | perm_x[(i + 1) & 255] << 8 (one load per axis)
+constexpr int kPerlinWords = 256 * 4 + 64 + 128;
+constexpr int kPerlinPermWord = 256 * 4, kPerlinPerm2Word = 256 * 4 + 64;
 
 // counter slots == RT_CNT_* (rt_render.h)
 enum : int {

@@ -67,15 +67,19 @@ std::vector<std::string> jit_extra_options() {
   return v;
 }
 
+// RT_JIT_WAVES=N asks the register allocator for N waves per SIMD (A/B; default: unconstrained)
+std::string waves_attr() {
+  if (const char *e = std::getenv("RT_JIT_WAVES"))
+    if (std::atoi(e) > 0) return " __attribute__((amdgpu_waves_per_eu(" + std::to_string(std::atoi(e)) + ")))";
+  return "";
+}
+
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
                 bool *folded) {
   std::string trace;
   if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
   const int v = variant & kJitVarMask;
-  // RT_JIT_WAVES=N asks the register allocator for N waves per SIMD (A/B; default: unconstrained)
-  std::string attr;
-  if (const char *e = std::getenv("RT_JIT_WAVES"))
-    if (std::atoi(e) > 0) attr = " __attribute__((amdgpu_waves_per_eu(" + std::to_string(std::atoi(e)) + ")))";
+  const std::string attr = waves_attr();
   *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
          "extern \"C\" __global__ __launch_bounds__(256)" + attr + " void rt_static_render(RenderArgs A) {\n"
          "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
@@ -317,7 +321,7 @@ std::string jit_accel_source(const SceneImage &img, int variant) {
   const int v = variant & kJitVarMask;
   const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u>";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
-  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render(RenderArgs A) {\n  render_body<" +
+  src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr() + " void rt_accel_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v) + ", " + at + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render_count(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarCount) + ", " + at + ">(A);\n}\n";

@@ -90,11 +90,14 @@ struct Compiler {
             perlin[base + 4 * i + 1] = fbits(p.gradients[i].y);
             perlin[base + 4 * i + 2] = fbits(p.gradients[i].z);
           }
-          uint8_t *perm = reinterpret_cast<uint8_t *>(perlin.data() + base + 256 * 4);
+          uint8_t *perm = reinterpret_cast<uint8_t *>(perlin.data() + base + kPerlinPermWord);
+          uint16_t *perm2 = reinterpret_cast<uint16_t *>(perlin.data() + base + kPerlinPerm2Word);
           for (int i = 0; i < RTR_PERLIN_POINTS; ++i) {
             if (p.perm_x[i] < 0 || p.perm_x[i] > 255) return -1;   // the gather index must stay in the table
             perm[i] = static_cast<uint8_t>(p.perm_x[i]);
           }
+          for (int i = 0; i < RTR_PERLIN_POINTS; ++i)
+            perm2[i] = static_cast<uint16_t>(perm[i] | (perm[(i + 1) & 255] << 8));
           perlin_index[po] = pidx;
         }
         w[T_PERLIN] = pidx;
