@@ -29,7 +29,7 @@ HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp 
 HIP_HDR  := $(wildcard $(CSRC)/*.h) $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h \
             $(CSRC)/device/embedded_headers.inc include/rt_render.h include/rt_ref_layout.h
 
-all: host hip oracle cli
+all: host hip oracle cli ref
 
 host: $(LIBDIR)/librt_host.so
 hip: $(LIBDIR)/librt_hip.so
@@ -57,6 +57,14 @@ bin/raytracing: $(CSRC)/host/cli.cpp $(LIBDIR)/librt_host.so $(LIBDIR)/librt_hip
 	$(CXX) $(HOST_FLAGS) $(INC) $(CSRC)/host/cli.cpp -o $@ -L$(LIBDIR) -lrt_host -lrt_hip \
 	  -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)'
 
+# reference-side checker (test infrastructure): the reference's stb_image compiled where it lies, only
+# when the reference tree is present (not on the GPU box); output only into oracle/_ref/
+REF_INC ?= /root/reference/include
+ref:
+	@if [ -f $(REF_INC)/stb_image.h ]; then mkdir -p oracle/_ref && \
+	  $(CXX) -O2 -fPIC -shared -w -I$(REF_INC) oracle/stbi_ref.cpp -o oracle/_ref/libstbi_ref.so; \
+	  else echo "ref: $(REF_INC)/stb_image.h not present, skipping oracle/_ref"; fi
+
 kat:
 	$(CXX) -O1 -std=c++17 -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include oracle/kat/gen_rocrand_kat.cpp \
 	  -o oracle/_build/gen_rocrand_kat -L$(ROCM)/lib -lamdhip64 -Wno-deprecated-declarations
@@ -65,4 +73,4 @@ kat:
 clean:
 	rm -rf $(LIBDIR)/*.so oracle/_build bin
 
-.PHONY: all host hip oracle cli kat clean
+.PHONY: all host hip oracle cli ref kat clean

@@ -10,12 +10,42 @@ from __future__ import annotations
 
 import ctypes as C
 import struct
+from pathlib import Path
 
 import numpy as np
 import pytest
 
 import cuda_raytracing_amd as rt
 from cuda_raytracing_amd import _abi
+
+
+REF_STBI = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "libstbi_ref.so"
+
+
+def stbi_loadf(path):
+    """The reference's own loader (stb_image v2.30 compiled where it lies, oracle/stbi_ref.cpp)."""
+    L = C.CDLL(str(REF_STBI))
+    L.rt_ref_stbi_loadf.restype = C.POINTER(C.c_float)
+    L.rt_ref_stbi_loadf.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.rt_ref_stbi_free.argtypes = [C.c_void_p]
+    w, h = C.c_int(0), C.c_int(0)
+    p = L.rt_ref_stbi_loadf(str(path).encode(), C.byref(w), C.byref(h))
+    if not p:
+        return None
+    try:
+        return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
+    finally:
+        L.rt_ref_stbi_free(p)
+
+
+def check_vs_stb(path, got):
+    """Pinned against the reference's stb_image when oracle/_ref is built (make ref, needs /root/reference)."""
+    if not REF_STBI.exists():
+        return
+    ref = stbi_loadf(path)
+    assert (ref is None) == (got is None)
+    if ref is not None:
+        assert ref.shape == got.shape and np.array_equal(ref.view(np.uint32), got.view(np.uint32))
 
 
 def ldr_to_float(px: np.ndarray) -> np.ndarray:
@@ -41,6 +71,7 @@ def test_every_byte_value_converts_like_stb(tmp_path):
     f = tmp_path / "ramp.pgm"
     f.write_bytes(b"P5\n16 16\n255\n" + pic.tobytes())
     got = rt.load_image(f)
+    check_vs_stb(f, got)
     assert got.shape == (16, 16, 3) and got.dtype == np.float32
     assert np.array_equal(got.view(np.uint32), expect(pic).view(np.uint32))
     assert got[0, 0, 0] == 0.0 and got[-1, -1, 0] == 1.0
@@ -50,6 +81,7 @@ def test_ppm_p6_with_comments(tmp_path, picture):
     f = tmp_path / "a.ppm"
     f.write_bytes(b"P6\n# a comment\n7 5\n# another\n255\n" + picture.tobytes())
     got = rt.load_image(f)
+    check_vs_stb(f, got)
     assert np.array_equal(got.view(np.uint32), expect(picture).view(np.uint32))
 
 
@@ -77,6 +109,7 @@ def test_bmp(tmp_path, picture, bpp, top_down):
     f = tmp_path / "a.bmp"
     f.write_bytes(bmp_bytes(picture, bpp, top_down))
     got = rt.load_image(f)
+    check_vs_stb(f, got)
     assert np.array_equal(got.view(np.uint32), expect(picture).view(np.uint32))
 
 
@@ -91,11 +124,13 @@ def test_tga(tmp_path, picture, grey, top_first):
     f = tmp_path / "a.tga"
     f.write_bytes(hdr + body)
     got = rt.load_image(f)
+    check_vs_stb(f, got)
     assert np.array_equal(got.view(np.uint32), expect(pic).view(np.uint32))
 
 
 def test_missing_file_is_the_reference_failed_load(tmp_path):
     assert rt.load_image(tmp_path / "earthmap.jpg") is None
+    check_vs_stb(tmp_path / "earthmap.jpg", None)
     w = rt.World()
     m = w.image(str(tmp_path / "earthmap.jpg"))
     assert w.status() == 0 and m.kind == 0
@@ -133,3 +168,23 @@ def test_earth_scene_loads_its_texture(tmp_path, monkeypatch, picture):
     arena = np.frombuffer(C.string_at(sc.textures, sc.texture_bytes), np.uint8)
     want = expect(picture).tobytes()
     assert arena.tobytes().find(want) > 0
+
+
+@pytest.mark.skipif(not REF_STBI.exists(), reason="oracle/_ref not built (needs /root/reference)")
+def test_reference_loader_is_pinned_on_random_images(tmp_path):
+    # random sizes and pixels through every decoded format, against stbi_loadf itself
+    rng = np.random.default_rng(11)
+    for case in range(12):
+        h, w = (int(x) for x in rng.integers(1, 40, size=2))
+        pic = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+        files = {
+            "a.ppm": b"P6 %d %d 255\n" % (w, h) + pic.tobytes(),
+            "a.pgm": b"P5\n%d %d\n255\n" % (w, h) + pic[:, :, 1].tobytes(),
+            "a.bmp": bmp_bytes(pic, 24 if case % 2 else 32, bool(case % 3 == 0)),
+        }
+        for name, data in files.items():
+            f = tmp_path / f"{case}_{name}"
+            f.write_bytes(data)
+            got = rt.load_image(f)
+            ref = stbi_loadf(f)
+            assert ref is not None and np.array_equal(ref.view(np.uint32), got.view(np.uint32)), f
