@@ -376,6 +376,9 @@ __device__ uint32_t texture_code(const Mem<LDS> &S, const RenderArgs &A, uint32_
       case T_NOISE: {
         if (!NOISE || !(TM & (1u << T_NOISE))) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
         if (COUNT) perlin_count++;
+#ifdef RT_DBG_CHEAP_NOISE   // timing experiment only (RT_JIT_OPTS): the paths do not depend on albedo
+        return __float_as_uint(0.5f);
+#endif
         const uint32_t tb = A.off_perlin + t0.y * kPerlinWords;
         float accum = 0.0f, weight = 1.0f;
         f3 q = p;
@@ -1034,6 +1037,53 @@ struct PacketTrace {
   }
 };
 
+// ---------------------------------------------------------------------------------------------
+// cooperative Perlin turbulence (perlin_noise.cpp:72-85 through texture_get_color's noise case,
+// raytracing.cu:386-395): the 7 octaves of the lanes in M spread over K lanes each
+// ---------------------------------------------------------------------------------------------
+// Lane L serves the noise lane of rank L / K (the (L / K)-th set bit of M) and evaluates its octaves
+// o = L % K, L % K + K, ... < 7 at q = p * 2^o — bit-identical to the reference's repeated doubling
+// (scaling by a power of two is exact, and overflows exactly when the doubling does).  Each noise lane
+// then gathers its 7 values and sums them in the reference's order.  Every lane of the wave must be
+// active.  Returns the colour-stack code of the attenuation for the lanes in M (unused elsewhere).
+template <int K, bool LDS>
+__device__ __forceinline__ uint32_t coop_noise_code(const Mem<LDS> &S, const RenderArgs &A, uint64_t M, uint32_t lane,
+                                                    uint64_t lt_mask, f3 p, uint32_t tb, float scale) {
+  const uint32_t grp = lane / K, slot = lane % K;
+  uint32_t pos = 0, r = grp;   // select the grp-th set bit of M
+#pragma unroll
+  for (uint32_t s = 32; s >= 1; s >>= 1) {
+    const uint32_t c = static_cast<uint32_t>(__popcll((M >> pos) & ((1ull << s) - 1ull)));
+    if (r >= c) { r -= c; pos += s; }
+  }
+  const bool serve = grp < static_cast<uint32_t>(__popcll(M));
+  const int own = static_cast<int>(serve ? pos : lane);
+  const float px = __shfl(p.x, own), py = __shfl(p.y, own), pz = __shfl(p.z, own);
+  const uint32_t otb = static_cast<uint32_t>(__shfl(static_cast<int>(tb), own));
+  constexpr int NI = (7 + K - 1) / K;
+  float nv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const uint32_t o = slot + static_cast<uint32_t>(i * K);
+    nv[i] = 0.0f;
+    if (serve && o < 7u) {
+      const float sc = __uint_as_float((127u + o) << 23);   // 2^o
+      nv[i] = perlin_noise(S, otb, mk(px * sc, py * sc, pz * sc));
+    }
+  }
+  const int rank = static_cast<int>(__popcll(M & lt_mask));
+  float accum = 0.0f, weight = 1.0f;
+#pragma unroll
+  for (int o = 0; o < 7; ++o) {
+    accum += weight * __shfl(nv[o / K], rank * K + (o % K));
+    weight *= 0.5f;
+  }
+  const float turb = fabsf(accum);
+  const float sv = 1 + rt_sinf(scale * p.z + 10 * turb);
+  const uint32_t g = __float_as_uint(0.5f * sv);
+  return ((g & kRcRecTag) == kRcRecTag) ? (kRcRecTag | (A.rc_consts + RC_NAN)) : g;
+}
+
 // linear -> P6 byte of pixels_to_ppm (raytracing.cu:1391-1395, 1419-1431): sqrt gamma (0 for
 // non-positive), clamp to [0, 0.999], (u8)(256 x) — the conversion of rt_tonemap / tonemap_kernel
 __device__ __forceinline__ uint8_t ppm_byte(float c) {
@@ -1259,14 +1309,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       ph_trace += t - t_mark;
       t_mark = t;
     }
-    if (!busy) continue;
-    probe_rounds++;
-
-    // ---- shade (ray_color loop body, :1340-1359) ----
+    // ---- shade (ray_color loop body, :1340-1359); lanes without a pixel only help the cooperative
+    // noise evaluation below ----
     bool done = false;
     f3 res = mk(0, 0, 0);
     f3 ruv = mk(0, 0, 0);
-    if (T.result) {
+    if (busy) probe_rounds++;
+    if (busy && T.result) {
       // cuda_material_scatter: random_test first, then the unit vector by rejection, drawn (z, y, x)
       // (:497-502, vec3.h:152-161) — for every material, lights included.  With A.max_tries > 0 a lane
       // whose tries all fail keeps its hit and resumes the rejection next round (skipping that round's
@@ -1312,7 +1361,34 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       ph_rej += t - t_mark;
       t_mark = t;
     }
-    if (T.result && !pending) {
+    // ---- cooperative noise (kernels with noise textures): a lane shading a Lambertian noise texture
+    // spends most of its round in the 7 octaves of perlin_turbulence — a trapped-path straggler, alone
+    // on its SIMD at the end of the frame, issues them one after the other.  When at most half of the
+    // wave needs one, the octaves are spread over 2, 4 or 8 lanes per noise lane (coop_noise_code) ----
+    bool coop = false;
+    uint32_t coop_code = 0;
+    if (NOISE && !COUNT && (TM & (1u << T_NOISE))) {
+      bool nz = false;
+      uint32_t ntb = 0;
+      float nsc = 0.0f;
+      if (busy && T.result && !pending) {
+        const uint4 mm = S.w4(A.off_mats + h.mat * kMatWords);
+        if (mm.x == MAT_LAMBERTIAN) {
+          const uint4 t0 = S.w4(A.off_texs + mm.y * kTexWords);
+          if (t0.x == T_NOISE) { nz = true; ntb = A.off_perlin + t0.y * kPerlinWords; nsc = asf(t0.w); }
+        }
+      }
+      const uint64_t nm = __ballot(nz);
+      const uint32_t nb = static_cast<uint32_t>(__popcll(nm));
+      if (nb != 0 && nb <= A.coop_noise && __ballot(true) == ~0ull) {
+        // (the 2-lane share costs 17 VGPRs, 4 -> 3 waves/SIMD, and still wins 3 % on scenes 17 and 19)
+        if (nb <= 8) coop_code = coop_noise_code<8>(S, A, nm, lane, lt_mask, h.p, ntb, nsc);
+        else if (nb <= 16) coop_code = coop_noise_code<4>(S, A, nm, lane, lt_mask, h.p, ntb, nsc);
+        else coop_code = coop_noise_code<2>(S, A, nm, lane, lt_mask, h.p, ntb, nsc);
+        coop = nz;
+      }
+    }
+    if (busy && T.result && !pending) {
       const uint32_t mbase = A.off_mats + h.mat * kMatWords;
       const uint4 m0 = S.w4(mbase), m1 = S.w4(mbase + 4);
       const uint32_t mkind = m0.x;
@@ -1332,7 +1408,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         dir = add(hn, ruv);
         const float eps = 1e-8f;
         if (fabsf(dir.x) < eps && fabsf(dir.y) < eps && fabsf(dir.z) < eps) dir = hn;
-        code = texture_code<LDS, COUNT, NOISE, UV, TM, WIDE>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
+        code = coop ? coop_code : texture_code<LDS, COUNT, NOISE, UV, TM, WIDE>(S, A, m0.y, h.u, h.v, h.p, c_perlin);
       } else if ((MM & (1u << MAT_METAL)) && mkind == MAT_METAL) {         // :466-472
         f3 rd = sub(ray.d, scale(2.0f * dot(ray.d, hn), hn));
         dir = add(unit(rd), scale(asf(m1.y), ruv));
@@ -1379,7 +1455,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         done = true;
         res = emit;
       }
-    } else if (!T.result) {
+    } else if (busy && !T.result) {
       done = true;
       res = mk(A.bg[0], A.bg[1], A.bg[2]);
     }

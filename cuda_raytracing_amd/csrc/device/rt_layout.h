@@ -166,6 +166,8 @@ struct RenderArgs {
                                   // wave still need a try (they resume next round; 0 = never early)
   uint32_t black_skip;            // every attenuation is finite (host-checked): a path ending in
                                   // (0,0,0) unwinds to +0 without reading its colour stack
+  uint32_t coop_noise;            // noise kernels: spread perlin_turbulence's octaves over the wave's lanes
+                                  // when at most this many (<= 32) lanes need one (0 = never)
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

@@ -164,7 +164,10 @@ struct rt_context {
   bool black_skip = false;                      // attenuations_finite(img) (RT_BLACK_SKIP=0 disables)
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
-  uint32_t prio_chunk = 64;                     // RT_PRIO_CHUNK: those tiles handed out in pieces of this many pixels
+  int prio_chunk = -1;                          // RT_PRIO_CHUNK: those tiles handed out in pieces of this many pixels
+                                                // (-1 auto: 1 with cooperative noise, else whole tiles)
+  uint32_t coop_noise = 32;                     // RT_COOP_NOISE: cooperative noise octaves when <= this many lanes
+                                                // of a wave need one (0 = never, max 32)
   uint32_t defer_lanes = 4;                     // RT_DEFER_LANES: end a round's rejection at <= this many lanes
   uint32_t defer_trace = 16, trace_min_iters = 16;  // RT_DEFER_TRACE, RT_TRACE_MIN (paused per-lane walks)
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
@@ -270,9 +273,10 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
+  if (const char *e = std::getenv("RT_COOP_NOISE")) c->coop_noise = static_cast<uint32_t>(std::min(32, std::max(0, std::atoi(e))));
   if (const char *e = std::getenv("RT_PRIO_CHUNK")) {
     const int v = std::atoi(e);
-    c->prio_chunk = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? static_cast<uint32_t>(v) : 64u;
+    c->prio_chunk = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 64;
   }
   if (const char *e = std::getenv("RT_DEFER_TRACE")) c->defer_trace = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
@@ -548,6 +552,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.reverse_tiles = c->sched == 2 ? 1u : 0u;
   a.fold_violation = static_cast<uint32_t *>(c->work.p) + 15;   // zeroed with the work counters
   a.black_skip = c->black_skip ? 1u : 0u;
+  a.coop_noise = c->coop_noise;
   a.max_tries = c->max_tries;
   a.defer_lanes = c->defer_lanes;
   a.defer_trace = c->defer_trace;
@@ -598,7 +603,13 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
     const int pt = c->prio_tiles >= 0 ? c->prio_tiles : kPrioTiles;
     a.prio_ids = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(pt) * 64u, a.n_ids));
-    a.prio_chunk = a.prio_ids ? c->prio_chunk : 64u;
+    // The costliest tiles of a noise scene hold pixels whose paths are trapped between noise surfaces
+    // (the Perlin scene's contact point: ~35k serial rounds per pixel); handed out one pixel at a time
+    // they spread over many waves, each with few noise lanes, whose octaves the idle lanes then share
+    // (measured on scene 17, d50, spp 1024: 204 ms whole tiles without cooperation, 168 with, 135 with
+    // single pixels; scene 0 and Cornell lose 4-10 % with split tiles, so they keep whole tiles)
+    const int pcn = c->prio_chunk >= 0 ? c->prio_chunk : ((c->img.has_noise && c->coop_noise) ? 1 : 64);
+    a.prio_chunk = a.prio_ids ? static_cast<uint32_t>(pcn) : 64u;
   }
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)

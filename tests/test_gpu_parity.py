@@ -660,3 +660,21 @@ def test_code_object_disk_cache(tmp_path):
     assert "End-to-end:" in outs[1][0]
     assert outs[0][1] and outs[0][1] == outs[1][1]
     assert list((tmp_path / "cache").glob("rt_*.co"))
+
+
+@pytest.mark.parametrize("idx", [17, 19])
+@pytest.mark.parametrize("env", [{}, {"RT_COOP_NOISE": "0"}, {"RT_COOP_NOISE": "8", "RT_PRIO_CHUNK": "64"},
+                                 {"RT_PRIO_CHUNK": "8"}])
+def test_cooperative_noise_octaves_vs_oracle(idx, env, monkeypatch):
+    # noise scenes: perlin_turbulence's octaves spread over 2/4/8 lanes per noise lane (render_body's
+    # cooperative block), the costliest tiles handed out pixel by pixel — the frame is the oracle's
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, 192, 108)
+    p = rt.make_params(s, W, H, spp=16, bounces=50)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_STATIC
+    assert np.array_equal(bits(fb), bits(ref))
