@@ -798,22 +798,26 @@ __device__ __forceinline__ bool accel_box(const Trav &T, const SlabRay &R, float
 }
 
 // sphere branch of hit() with the record commit of sphere_hit<UV>; also reports a root equal to tmax.
-// a = dot(d, d), 4 * a and 2 * a are the same for every sphere of the walk (the ray is not transformed
-// in an all-sphere world): computed once per ray by the caller, the same IEEE operations.
-template <bool UV>
+// a = dot(d, d) and 2 * a are the same for every sphere of the walk (the ray is not transformed in an
+// all-sphere world): computed once per ray by the caller, the same IEEE operations.
+// FAST: the roots' division by 2a goes through the ray's reciprocal ra2 = rcp_ref(2a) (div_ref, exact
+// when 2a is in [2^-40, 2^60]: the numerator -b -+ sqrt(disc) of a walkable ray is below 2^43 in
+// magnitude, so the exponent gap stays < 96 and the quotient normal; a numerator too small for
+// div_ref's preconditions gives a quotient below 2^-86, rejected as < tmin either way).
+template <bool UV, bool FAST>
 __device__ __forceinline__ bool sphere_hit_tie(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
-                                               float inv_rad, float a4, float a2, bool &tie) {
+                                               float inv_rad, float a2, float ra2, bool &tie) {
   f3 center = line_at(c0, r.time, mv);
   f3 oc = sub(center, r.o);
   float b = -2.0f * dot(r.d, oc);
   float c = dot(oc, oc) - rad2;
-  float disc = b * b - a4 * c;
+  float disc = b * b - (2.0f * a2) * c;   // 4 * a == 2 * (2 * a) exactly
   if (!(disc >= 0)) return false;
   float sq = sqrtf(disc);
-  float root = (-b - sq) / a2;
+  float root = FAST ? div_ref(-b - sq, a2, ra2) : (-b - sq) / a2;
   tie |= root == T.tmax;
   if (kTmin >= root || root >= T.tmax) {
-    root = (-b + sq) / a2;
+    root = FAST ? div_ref(-b + sq, a2, ra2) : (-b + sq) / a2;
     tie |= root == T.tmax;
   }
   if (!(kTmin < root && root < T.tmax)) return false;
@@ -848,7 +852,10 @@ struct AccelTraceK {
     const float dmax = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
     // bounded, finite rays with no tiny direction component (finite 1/dir); the counting variant
     // walks the reference tree so that the op model counts the reference's visits
-    const bool nice = !COUNT && (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f);
+    // (and 2|d|^2 >= 2^-40, so that the roots' division by 2a can use the ray's reciprocal, sphere_hit_tie)
+    // (and max |d_i| >= 7e-7, so 2|d|^2 >= 2^-40 and the roots' division by 2a can use the ray's
+    // reciprocal, sphere_hit_tie)
+    const bool nice = !COUNT && (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f) && (dmax >= 7.0e-7f);
     bool tie = resume && T.atie != 0;
     uint32_t best = resume ? T.abest : 0u;
     const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
@@ -859,7 +866,8 @@ struct AccelTraceK {
       const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
       const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
       const SlabRay sr = slab_ray(T, oinv, pinv);
-      const float sa = dot(r.d, r.d), sa4 = 4 * sa, sa2 = 2.0f * sa;   // sphere_hit_tie's per-ray terms
+      const float sa2 = 2.0f * dot(r.d, r.d);   // sphere_hit_tie's per-ray terms
+      const float sra2 = rcp_ref(sa2);
       uint32_t node = resume ? T.anode : A.accel_root;
       int sp = resume ? T.asp : 0;
       // Wave-uniform loop, one node per walking lane per step.  Rays differ wildly in length (the
@@ -885,8 +893,8 @@ struct AccelTraceK {
         for (uint32_t k = 0; k < c1 + c2; ++k) {
           const uint32_t pr = (k < c1 ? f1 : f2) + k;
           const uint4 p0 = P[pr * 4], p1 = P[pr * 4 + 1], p2 = P[pr * 4 + 2];
-          if (sphere_hit_tie<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
-                                 asf(p1.z), asf(p1.w), sa4, sa2, tie))
+          if (sphere_hit_tie<UV, true>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
+                                       asf(p1.z), asf(p1.w), sa2, sra2, tie))
             best = pr;
         }
         hn = hn && !ln;
@@ -1309,8 +1317,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       ph_trace += t - t_mark;
       t_mark = t;
     }
-    // ---- shade (ray_color loop body, :1340-1359); lanes without a pixel only help the cooperative
-    // noise evaluation below ----
+    // ---- shade (ray_color loop body, :1340-1359); in noise kernels lanes without a pixel stay to help
+    // the cooperative noise evaluation below ----
+    if (!NOISE && !busy) continue;
     bool done = false;
     f3 res = mk(0, 0, 0);
     f3 ruv = mk(0, 0, 0);
