@@ -660,33 +660,38 @@ __device__ __forceinline__ void rotate_exit_dir(Trav &T, Ray &r, Hit &h, float s
 // ---------------------------------------------------------------------------------------------
 // One iteration of hit()'s while loop (:1089-1249): pop one record and process it.
 // KM: kinds that can occur in the scene (bit K_*); the run-time compiled lane kernels drop the others
-template <bool LDS, bool COUNT, bool UV, uint32_t KM = 0x7fu>
+// ALL: load the whole 80-B record at once (one memory latency per step instead of the kind word, then
+// the rest: the main per-lane walk of large scenes); the verified walk's rare fallback keeps the
+// two-step load, which needs fewer registers
+template <bool LDS, bool COUNT, bool UV, uint32_t KM = 0x7fu, bool ALL = true>
 __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hit &h, uint16_t *stk, Visits &vc) {
   int sp = T.sp - 1;
   const uint32_t idx = stk[sp * 64];
   const uint32_t nb = idx * kNodeWords;
   const uint4 w0 = S.w4(nb);
+  uint4 w1, w2, w3, w4;
+  if (ALL) { w1 = S.w4(nb + 4); w2 = S.w4(nb + 8); w3 = S.w4(nb + 12); w4 = S.w4(nb + 16); }
   const uint32_t kind = w0.x;
   if (COUNT) { vc.k[kind < 7 ? kind : 0]++; }
   const bool in_xf = T.tc || T.yc;
   if ((KM & (1u << K_BVH)) && kind == K_BVH) {                             // :1124-1130
-    const uint4 w1 = S.w4(nb + 4);
+    if (!ALL) w1 = S.w4(nb + 4);
     if (box_hit(T, r, asf(w0.z), asf(w0.w), asf(w1.x), asf(w1.y), asf(w1.z), asf(w1.w))) {
       stk[sp * 64] = static_cast<uint16_t>(w0.y >> 16);      // right
       stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);      // left (popped first)
       sp += 2;
     }
   } else if ((KM & ((1u << K_QUAD) | (1u << K_TRIANGLE))) && (kind == K_QUAD || kind == K_TRIANGLE)) {
-    const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8), w3 = S.w4(nb + 12), w4 = S.w4(nb + 16);
+    if (!ALL) { w1 = S.w4(nb + 4); w2 = S.w4(nb + 8); w3 = S.w4(nb + 12); w4 = S.w4(nb + 16); }
     planar_hit(T, r, h, kind == K_TRIANGLE, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), asf(w1.y),
                mk(asf(w1.z), asf(w1.w), asf(w2.x)), mk(asf(w2.y), asf(w2.z), asf(w2.w)),
                mk(asf(w3.x), asf(w3.y), asf(w3.z)), mk(asf(w3.w), asf(w4.x), asf(w4.y)), in_xf);
   } else if ((KM & (1u << K_SPHERE)) && kind == K_SPHERE) {
-    const uint4 w1 = S.w4(nb + 4), w2 = S.w4(nb + 8);
+    if (!ALL) { w1 = S.w4(nb + 4); w2 = S.w4(nb + 8); }
     sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
                    asf(w2.y), asf(w2.z), in_xf);
   } else if ((KM & (1u << K_TRANSLATE)) && kind == K_TRANSLATE) {
-    const uint4 w1 = S.w4(nb + 4);
+    if (!ALL) w1 = S.w4(nb + 4);
     const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
     if (T.tc == 0) {
       translate_enter(T, r, off);
@@ -721,7 +726,7 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
 // PAUSE: the walk may stop at the end of a round with its state kept in T and the LDS stack (as in
 // AccelTraceK: the round's walk ends once at most A.defer_trace lanes, <= 1/4 of the starters, are
 // still walking after A.trace_min_iters steps); the walk resumes next round with shading skipped.
-template <uint32_t KM, bool PAUSE = false>
+template <uint32_t KM, bool PAUSE = false, bool ALL = true>
 struct LaneTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t, uint32_t,
@@ -733,12 +738,12 @@ struct LaneTraceK {
       T.sp = 1;
     }
     if (!PAUSE) {
-      while (T.sp > 0) trav_step<LDS, COUNT, UV, KM>(S, T, r, h, stk, vc);
+      while (T.sp > 0) trav_step<LDS, COUNT, UV, KM, ALL>(S, T, r, h, stk, vc);
       return;
     }
     const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(true)));
     for (uint32_t it = 1;; ++it) {
-      if (T.sp > 0) trav_step<LDS, COUNT, UV, KM>(S, T, r, h, stk, vc);
+      if (T.sp > 0) trav_step<LDS, COUNT, UV, KM, ALL>(S, T, r, h, stk, vc);
       const uint64_t left = __ballot(T.sp > 0);
       if (left == 0) break;
       const uint32_t nl = static_cast<uint32_t>(__popcll(left));
@@ -942,7 +947,7 @@ struct AccelTraceK {
     if (fb != 0) {   // rare: the reference walk for those lanes
       asm volatile("" ::: "memory");
       if (!COUNT && lane == static_cast<uint32_t>(__builtin_ctzll(fb))) atomicAdd(A.accel_fallbacks, static_cast<uint32_t>(__popcll(fb)));
-      LaneTraceK<KM>::template run<LDS, COUNT, UV>(S, A, need_ref, lanes, lane, stk, T, r, h, vc);
+      LaneTraceK<KM, false, false>::template run<LDS, COUNT, UV>(S, A, need_ref, lanes, lane, stk, T, r, h, vc);
     }
   }
 };
