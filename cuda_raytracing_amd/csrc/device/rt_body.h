@@ -246,10 +246,6 @@ __device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
   float wu[2] = {1 - uu, uu}, wv[2] = {1 - vv, vv}, wwk[2] = {1 - ww, ww};
   float du[2] = {u, u - 1.0f}, dv[2] = {v, v - 1.0f}, dw[2] = {w, w - 1.0f};
   uint32_t pi[2] = {pi0, pi1}, pj[2] = {pj0, pj1}, pk[2] = {pk0, pk1};
-  // the eight gradient gathers are issued before the arithmetic
-  uint4 gr[8];
-#pragma unroll
-  for (int c8 = 0; c8 < 8; ++c8) gr[c8] = S.w4(tb + 4 * ((pi[c8 >> 2] ^ pj[(c8 >> 1) & 1] ^ pk[c8 & 1]) & 255));
   float accum = 0.0f;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -257,8 +253,9 @@ __device__ float perlin_noise(const Mem<LDS> &S, uint32_t tb, f3 p) {
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const uint4 g = gr[4 * a + 2 * b + c];
-        f3 grad = mk(asf(g.x), asf(g.y), asf(g.z));
+        uint32_t g = (pi[a] ^ pj[b] ^ pk[c]) & 255;
+        uint4 gr = S.w4(tb + 4 * g);
+        f3 grad = mk(asf(gr.x), asf(gr.y), asf(gr.z));
         accum += wu[a] * wv[b] * wwk[c] * dot(grad, mk(du[a], dv[b], dw[c]));
       }
   return accum;
@@ -1120,6 +1117,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   constexpr bool NOISE = (F & kVarNoise) != 0, UV = (F & kVarUv) != 0;
   constexpr bool TRACE = (F & kVarTrace) != 0;   // per-wave timeline into A.wave_trace (diagnostics)
   constexpr bool DEEP = (F & kVarDeep) != 0;     // batched unwind of HBM colour-stack levels
+  constexpr bool COOP = NOISE && (F & kVarCoop) != 0;   // cooperative noise octaves
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
   Mem<LDS> S{A.scene};
@@ -1324,7 +1322,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     // ---- shade (ray_color loop body, :1340-1359); in noise kernels lanes without a pixel stay to help
     // the cooperative noise evaluation below ----
-    if (!NOISE && !busy) continue;
+    if (!COOP && !busy) continue;
     bool done = false;
     f3 res = mk(0, 0, 0);
     f3 ruv = mk(0, 0, 0);
@@ -1381,7 +1379,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     // wave needs one, the octaves are spread over 2, 4 or 8 lanes per noise lane (coop_noise_code) ----
     bool coop = false;
     uint32_t coop_code = 0;
-    if (NOISE && !COUNT && (TM & (1u << T_NOISE))) {
+    if (COOP && !COUNT && (TM & (1u << T_NOISE))) {
       bool nz = false;
       uint32_t ntb = 0;
       float nsc = 0.0f;

@@ -100,9 +100,12 @@ constexpr int kDeepBounces = 16;
 // run-time compiled kernels whose colour-stack codes fit 16 bits (no noise, no texels, < 65536 colour
 // records): two levels per LDS word.  The offline kernels always use 32-bit codes.
 constexpr int kVarNarrow = 1 << 15;
+// run-time compiled scene-specialised kernels of noise scenes: cooperative noise octaves (render_body);
+// the large-scene walks leave it out (its registers cost them a wave; noise is not their bottleneck)
+constexpr int kVarCoop = 1 << 16;
 // variant bits the run-time compiled kernels are specialised on
-constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | (15 << kVarMatShift) |
-                            (15 << kVarTexShift);
+constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop |
+                            (15 << kVarMatShift) | (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling

@@ -416,7 +416,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     std::string why;
     const bool want_fold = c->fold_enabled && !(p->flags & RT_FLAG_NO_FOLD) &&
                            ray_bound(c->img, cam, p) <= kFoldRayBound;
-    if (rt::jit_kernels(c->img, c->variant | trace_bit, c->jit_budget, want_fold, &jk, &why)) {
+    if (rt::jit_kernels(c->img, c->variant | trace_bit | (c->img.has_noise ? rt::kVarCoop : 0), c->jit_budget, want_fold,
+                        &jk, &why)) {
       note_jit(jk);
       c->used_fold = jk.folded;
       jit_fn = c->counted ? jk.render_count : jk.render;
@@ -767,7 +768,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
   std::string src;
   if (traversal == RT_TRAV_STATIC) {
     uint32_t v = 0;
-    if (!rt::jit_source(img, variant, 256, true, &src, &v)) return RT_ERR_UNSUPPORTED;
+    if (!rt::jit_source(img, variant | (img.has_noise ? rt::kVarCoop : 0), 256, true, &src, &v)) return RT_ERR_UNSUPPORTED;
   } else if (traversal == RT_TRAV_ACCEL) {
     rt::SphereAccel a;
     std::string why;
