@@ -1254,11 +1254,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       if (need && rank < avail) {
         // tile-major id -> (local row, column); ids past the shard edge are skipped
         const uint32_t id = chunk_pos + rank;
-        uint32_t tile, k;
-        if (A.probe_cost) {                 // probe: probe_per_tile distinct pixels spread over the tile
+        uint32_t tile, k, salt = 0;
+        if (A.probe_cost) {                 // probe: probe_per_tile paths spread over the tile's pixels
           tile = id / A.probe_per_tile;
           const uint32_t q = id - tile * A.probe_per_tile;
-          k = (q * 37u + 11u) & 63u;
+          k = (q * 37u + 11u) & 63u;        // a permutation of the 64 pixels per 64 paths
+          salt = q >> 6;                    // more than 64 paths per tile: another stream per pixel
         } else {
           tile = id >> 6;
           k = id & 63u;
@@ -1274,7 +1275,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           if (A.probe_cost) {               // throwaway stream: the real ones are not consumed
             probe_tile = tile;
             probe_rounds = 0;
-            uint32_t hsh = static_cast<uint32_t>(pix) * 0x9E3779B9u + 0x7F4A7C15u;
+            uint32_t hsh = static_cast<uint32_t>(pix) * 0x9E3779B9u + 0x7F4A7C15u + salt * 0x632BE5ABu;
             hsh ^= hsh >> 16; hsh *= 0x85EBCA6Bu; hsh ^= hsh >> 13; hsh *= 0xC2B2AE35u; hsh ^= hsh >> 16;
             rng.d = hsh; rng.x0 = hsh ^ 0x2c7f967fu; rng.x1 = hsh * 3u + 1u; rng.x2 = ~hsh;
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;

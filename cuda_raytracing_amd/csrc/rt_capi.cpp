@@ -172,7 +172,7 @@ struct rt_context {
   uint32_t defer_trace = 16, trace_min_iters = 16;  // RT_DEFER_TRACE, RT_TRACE_MIN (paused per-lane walks)
   bool lane_jit = true;                         // RT_JIT_LANE=0: offline all-kinds lane kernel
   bool shade_spec = true;                       // RT_JIT_SHADE=0: run-time kernels keep every material
-  uint32_t probe_per_tile = 0;   // RT_PROBE (1..64); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
+  uint32_t probe_per_tile = 0;   // RT_PROBE (1..256); 0 = clamp(spp / 4, 8, 64) paths per 64-pixel tile
   bool used_lpt = false;
   bool fold_enabled = true;
   uint32_t fold_violations = 0;      // RT_JIT_FOLD=0 disables exact constant folding (A/B)
@@ -263,7 +263,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_SCHED")) c->sched = std::atoi(e);
   if (const char *e = std::getenv("RT_JIT_FOLD")) c->fold_enabled = e[0] != '0';
   if (const char *e = std::getenv("RT_PROBE"))
-    c->probe_per_tile = static_cast<uint32_t>(std::min(64, std::max(1, std::atoi(e))));
+    c->probe_per_tile = static_cast<uint32_t>(std::min(256, std::max(1, std::atoi(e))));
   if (const char *e = std::getenv("RT_RC_LDS_LEVELS")) {
     c->rc_lds_levels = static_cast<uint32_t>(std::atoi(e));
     c->rc_lds_auto = false;
