@@ -3,7 +3,7 @@
 // The reference loads texels with stb_image's stbi_loadf(file, &w, &h, &n, 3): three float channels per
 // texel, row 0 = the top row of the picture, 8-bit formats converted by pow(c / 255, 2.2) * 1 (stb_image's
 // default LDR->float gamma and scale).  stb_image itself is a third-party header that is not part of this
-// build; this file decodes the uncompressed formats it reads — binary PNM (P5 grey, P6 RGB; maxval <= 255),
+// build; this file decodes the uncompressed formats it reads — binary PNM (P5 grey, P6 RGB; 8 and 16 bit),
 // BMP (BI_RGB, 24 and 32 bit) and TGA (uncompressed true-colour and grey, 8/24/32 bit) — with the same
 // output convention.  A file that exists in another format (JPEG, PNG, ...) is RT_ERR_UNSUPPORTED; a file
 // that does not exist is the reference's failed load (no pixels: the texture renders magenta, :346-347).
@@ -65,7 +65,9 @@ float *to_float_rgb(const std::vector<uint8_t> &px, int w, int h, int comp) {
 
 bool dims_ok(uint64_t w, uint64_t h) { return w > 0 && h > 0 && w <= (1u << 24) && h <= (1u << 24) && w * h <= (1ull << 28); }
 
-// binary PNM: P5 / P6, maxval 1..255 (stbi__pnm_load)
+// binary PNM: P5 / P6 (stbi__pnm_info / stbi__pnm_load).  Samples are taken as stored, not rescaled by
+// maxval; maxval > 255 means two bytes per sample, which stb_image reads into native (little-endian) 16-bit
+// words and reduces with >> 8 (stbi__convert_16_to_8): the sample's second byte.
 int load_pnm(Reader &r, float **rgb, int32_t *w, int32_t *h) {
   if (!r.ok(2) || r.b[0] != 'P' || (r.b[1] != '5' && r.b[1] != '6')) return RT_ERR_UNSUPPORTED;
   const int comp = r.b[1] == '6' ? 3 : 1;
@@ -83,10 +85,11 @@ int load_pnm(Reader &r, float **rgb, int32_t *w, int32_t *h) {
   }
   if (!r.ok(1)) return RT_ERR_UNSUPPORTED;
   r.p++;   // the single whitespace after maxval
-  if (!dims_ok(v[0], v[1]) || v[2] == 0 || v[2] > 255) return RT_ERR_UNSUPPORTED;
-  const size_t bytes = v[0] * v[1] * comp;
-  if (!r.ok(bytes)) return RT_ERR_UNSUPPORTED;
-  std::vector<uint8_t> px(r.b.begin() + r.p, r.b.begin() + r.p + bytes);
+  if (!dims_ok(v[0], v[1]) || v[2] > 65535) return RT_ERR_UNSUPPORTED;
+  const size_t bps = v[2] > 255 ? 2 : 1, n = v[0] * v[1] * comp;
+  if (!r.ok(n * bps)) return RT_ERR_UNSUPPORTED;
+  std::vector<uint8_t> px(n);
+  for (size_t i = 0; i < n; ++i) px[i] = r.b[r.p + i * bps + bps - 1];
   *w = static_cast<int32_t>(v[0]);
   *h = static_cast<int32_t>(v[1]);
   *rgb = to_float_rgb(px, *w, *h, comp);

@@ -85,6 +85,21 @@ def test_ppm_p6_with_comments(tmp_path, picture):
     assert np.array_equal(got.view(np.uint32), expect(picture).view(np.uint32))
 
 
+@pytest.mark.parametrize("maxval", [0, 100, 256, 65535])
+def test_pnm_samples_are_taken_as_stored(tmp_path, picture, maxval):
+    # stb does not rescale by maxval; 16-bit samples (maxval > 255) come out as their second byte
+    if maxval > 255:
+        hi = np.random.default_rng(3).integers(0, 256, size=picture.shape, dtype=np.uint8)
+        body = np.stack([hi, picture], axis=-1).tobytes()
+    else:
+        body = picture.tobytes()
+    f = tmp_path / "a.ppm"
+    f.write_bytes(b"P6\n7 5\n%d\n" % maxval + body)
+    got = rt.load_image(f)
+    check_vs_stb(f, got)
+    assert np.array_equal(got.view(np.uint32), expect(picture).view(np.uint32))
+
+
 def bmp_bytes(pic: np.ndarray, bpp: int, top_down: bool) -> bytes:
     h, w, _ = pic.shape
     bypp = bpp // 8
@@ -137,7 +152,7 @@ def test_missing_file_is_the_reference_failed_load(tmp_path):
 
 
 @pytest.mark.parametrize("payload", [b"\xff\xd8\xff\xe0\x00\x10JFIF\x00", b"\x89PNG\r\n\x1a\n\x00\x00", b"P3\n1 1\n255\n0 0 0\n",
-                                     b"P6\n1 1\n65535\n\0\0\0\0\0\0"])
+                                     b"P6\n1 1\n65536\n\0\0\0\0\0\0", b"P6\n2 1\n255\n\0\0\0"])
 def test_other_formats_are_unsupported(tmp_path, payload):
     f = tmp_path / "earthmap.jpg"
     f.write_bytes(payload)
