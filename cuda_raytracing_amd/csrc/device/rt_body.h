@@ -806,7 +806,28 @@ __device__ __forceinline__ bool accel_box(const Trav &T, const SlabRay &R, float
 // when 2a is in [2^-40, 2^60]: the numerator -b -+ sqrt(disc) of a walkable ray is below 2^43 in
 // magnitude, so the exponent gap stays < 96 and the quotient normal; a numerator too small for
 // div_ref's preconditions gives a quotient below 2^-86, rejected as < tmin either way).
-template <bool UV, bool FAST>
+// The record of the accepted sphere is a function of (root, ray, sphere) only, so the walk commits it once
+// after the last step (sphere_commit, from the closest sphere's index) instead of at every acceptance:
+// the same operations on the same values, outside the loop.
+template <bool UV>
+__device__ __forceinline__ void sphere_commit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float inv_rad) {
+  const f3 center = line_at(c0, r.time, mv);
+  h.t = T.tmax;
+  h.p = line_at(r.o, h.t, r.d);
+  h.mat = mat;
+  f3 outward = scale(inv_rad, sub(h.p, center));
+  if (UV) {
+    const float pi = 3.1415926535897932385f;
+    float theta = rt_acosf(-outward.y);
+    float phi = rt_atan2f(-outward.z, outward.x) + pi;
+    h.u = phi / (2 * pi);
+    h.v = theta / pi;
+  }
+  h.fd = dot(r.d, outward);
+  h.n = outward;
+}
+
+template <bool UV, bool FAST, bool COMMIT = true>
 __device__ __forceinline__ bool sphere_hit_tie(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
                                                float inv_rad, float a2, float ra2, bool &tie) {
   f3 center = line_at(c0, r.time, mv);
@@ -823,6 +844,11 @@ __device__ __forceinline__ bool sphere_hit_tie(Trav &T, const Ray &r, Hit &h, ui
     tie |= root == T.tmax;
   }
   if (!(kTmin < root && root < T.tmax)) return false;
+  if (!COMMIT) {
+    T.tmax = root;
+    T.result = true;
+    return true;
+  }
   h.t = root;
   h.p = line_at(r.o, root, r.d);
   h.mat = mat;
@@ -895,7 +921,7 @@ struct AccelTraceK {
         for (uint32_t k = 0; k < c1 + c2; ++k) {
           const uint32_t pr = (k < c1 ? f1 : f2) + k;
           const uint4 p0 = P[pr * 4], p1 = P[pr * 4 + 1], p2 = P[pr * 4 + 2];
-          if (sphere_hit_tie<UV, true>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
+          if (sphere_hit_tie<UV, true, false>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
                                        asf(p1.z), asf(p1.w), sa2, sra2, tie))
             best = pr;
         }
@@ -927,6 +953,8 @@ struct AccelTraceK {
     T.active = 0;
     bool need_ref = !nice || tie;
     if (nice && T.result) {
+      const uint4 p0 = P[best * 4], p1 = P[best * 4 + 1], p2 = P[best * 4 + 2];
+      sphere_commit<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)), asf(p1.w));
       // (2): the hit point inside P's deepest reference BVH ancestor box with a margin of 2^-19 of
       // the magnitudes the slab test and the hit point round (|o|, |p|, |t d| per axis): the
       // reference's slab values err by <= 3u |x - o| and p by <= 2u (|o| + |t d|), u = 2^-24
