@@ -1162,8 +1162,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   uint16_t *stk = reinterpret_cast<uint16_t *>(g_lds + A.stack_lds_word) + wave * A.stack_cap * 64 + lane;
   // colour stack (codes, rt_layout.h): level k < rc_lds_levels in LDS, lane-interleaved (conflict-free) —
   // wide: rcw[k * 64]; narrow: two levels per word, rch[(k >> 1) * 128 + (k & 1)] (rc_lds_levels even) —
-  // deeper levels in HBM at rc[k * threads + gtid]
+  // deeper levels in HBM at rc[gtid * max_bounces + k]
   constexpr bool WIDE = (F & kVarNarrow) == 0;
+  const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
   uint32_t *rcw = g_lds + A.rc_lds_word + wave * A.rc_lds_levels * 64 + lane;
   uint16_t *rch = reinterpret_cast<uint16_t *>(g_lds + A.rc_lds_word + wave * (A.rc_lds_levels >> 1) * 64 + lane);
   auto rc_lds_store = [&](uint32_t k, uint32_t code) {
@@ -1173,17 +1174,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   auto rc_lds_load = [&](uint32_t k) -> uint32_t {
     return WIDE ? rcw[k * 64] : static_cast<uint32_t>(rch[(k >> 1) * 128 + (k & 1)]);
   };
+  // HBM levels lane-contiguous (rc[gtid * max_bounces + k]): a deep path's successive levels fill the same
+  // cache lines, which reach HBM whole instead of as one 4-byte piece per line
   auto rc_hbm_store = [&](uint32_t k, uint32_t code) {
-    const size_t i = static_cast<size_t>(k) * A.threads + gtid;
+    const size_t i = static_cast<size_t>(gtid) * mb + k;
     if (WIDE) static_cast<uint32_t *>(A.rc)[i] = code;
     else static_cast<uint16_t *>(A.rc)[i] = static_cast<uint16_t>(code);
   };
   auto rc_hbm_load = [&](uint32_t k) -> uint32_t {
-    const size_t i = static_cast<size_t>(k) * A.threads + gtid;
+    const size_t i = static_cast<size_t>(gtid) * mb + k;
     return WIDE ? static_cast<const uint32_t *>(A.rc)[i] : static_cast<uint32_t>(static_cast<const uint16_t *>(A.rc)[i]);
   };
   const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
 
   bool busy = false;                      // lane owns a pixel
   bool hot = false;                       // the pixel is one of the first A.prio_ids handed out

@@ -143,7 +143,7 @@ struct RenderArgs {
                               // k = 8 * row-in-tile + column-in-tile): a wave's 64 pixels are 256 B per word
   float *out;                 // [n_pixels][3]
   uint8_t *out8;              // optional [n_pixels][3] P6 payload bytes (pixels_to_ppm), null = none
-  void *rc;                   // colour-stack levels past the LDS ones: [max_bounces][threads] codes
+  void *rc;                   // colour-stack levels past the LDS ones: [threads][max_bounces] codes
                               // (u32, or u16 in narrow kernels)
   uint32_t threads;           // grid size in threads (rc stride)
   uint32_t *work;             // chunk counter (zeroed per launch)
