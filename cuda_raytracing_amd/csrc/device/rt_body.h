@@ -1176,13 +1176,20 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   };
   // HBM levels lane-contiguous (rc[gtid * max_bounces + k]): a deep path's successive levels fill the same
   // cache lines, which reach HBM whole instead of as one 4-byte piece per line
+  auto rc_at = [&](uint32_t k) -> size_t {
+#ifdef RT_RC_INTERLEAVED   // A/B: level-major (rc[k * threads + gtid])
+    return static_cast<size_t>(k) * A.threads + gtid;
+#else
+    return static_cast<size_t>(gtid) * mb + k;
+#endif
+  };
   auto rc_hbm_store = [&](uint32_t k, uint32_t code) {
-    const size_t i = static_cast<size_t>(gtid) * mb + k;
+    const size_t i = rc_at(k);
     if (WIDE) static_cast<uint32_t *>(A.rc)[i] = code;
     else static_cast<uint16_t *>(A.rc)[i] = static_cast<uint16_t>(code);
   };
   auto rc_hbm_load = [&](uint32_t k) -> uint32_t {
-    const size_t i = static_cast<size_t>(gtid) * mb + k;
+    const size_t i = rc_at(k);
     return WIDE ? static_cast<const uint32_t *>(A.rc)[i] : static_cast<uint32_t>(static_cast<const uint16_t *>(A.rc)[i]);
   };
   const uint64_t lt_mask = (1ull << lane) - 1ull;
