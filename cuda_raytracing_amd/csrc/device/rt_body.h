@@ -1146,6 +1146,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   constexpr bool TRACE = (F & kVarTrace) != 0;   // per-wave timeline into A.wave_trace (diagnostics)
   constexpr bool DEEP = (F & kVarDeep) != 0;     // batched unwind of HBM colour-stack levels
   constexpr bool COOP = NOISE && (F & kVarCoop) != 0;   // cooperative noise octaves
+  // schedule probe launch (1-spp throwaway paths, costs per tile): fixed at compile time in the run-time
+  // compiled kernels, read from RenderArgs::probe_cost in the offline ones
+  const bool probe = (F & kVarProbe) != 0 || ((F & kVarNoProbe) == 0 && A.probe_cost != nullptr);
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
   Mem<LDS> S{A.scene};
@@ -1216,6 +1219,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool prio_done = false;                  // wave-uniform: the split costliest tiles are all handed out
   uint32_t tiles_taken = 0, rounds = 0;
   uint32_t probe_tile = 0, probe_rounds = 0;
+  bool probe_end = false;                  // probe: the lane's path ended in the last round
   uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, ph_unwind = 0, ph_cam = 0, t_mark = 0;   // wave-trace clocks
   uint64_t busy_lane_rounds = 0;
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1262,6 +1266,22 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       if (t_mark) ph_shade += t - t_mark;
       t_mark = t;
     }
+    if (probe) {
+      // the lanes whose probe path ended last round add their rounds to their tile's cost: one atomic per
+      // tile, the rounds summed across the wave first (all lanes are active here)
+      uint64_t left = __ballot(probe_end);
+      while (left) {
+        const int leader = __builtin_ctzll(left);
+        const uint32_t t = __builtin_amdgcn_readfirstlane(__shfl(probe_tile, leader));
+        const bool mine = probe_end && probe_tile == t;
+        uint32_t v = mine ? probe_rounds : 0u;
+#pragma unroll
+        for (int sh = 1; sh < 64; sh <<= 1) v += __shfl_xor(v, sh);
+        if (lane == static_cast<uint32_t>(leader)) atomicAdd(A.probe_cost + t, v);
+        left &= ~__ballot(mine);
+      }
+      probe_end = false;
+    }
     // ---- lanes without a pixel take the next pixels of the wave's tile ----
     bool need = !busy;
     uint64_t m = __ballot(need);
@@ -1292,7 +1312,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         // tile-major id -> (local row, column); ids past the shard edge are skipped
         const uint32_t id = chunk_pos + rank;
         uint32_t tile, k, salt = 0;
-        if (A.probe_cost) {                 // probe: probe_per_tile paths spread over the tile's pixels
+        if (probe) {                        // probe: probe_per_tile paths spread over the tile's pixels
           tile = id / A.probe_per_tile;
           const uint32_t q = id - tile * A.probe_per_tile;
           k = (q * 37u + 11u) & 63u;        // a permutation of the 64 pixels per 64 paths
@@ -1309,7 +1329,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           need = false;
           busy = true;
           hot = id < A.prio_ids;
-          if (A.probe_cost) {               // throwaway stream: the real ones are not consumed
+          if (probe) {                      // throwaway stream: the real ones are not consumed
             probe_tile = tile;
             probe_rounds = 0;
             uint32_t hsh = static_cast<uint32_t>(pix) * 0x9E3779B9u + 0x7F4A7C15u + salt * 0x632BE5ABu;
@@ -1566,8 +1586,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       sum = add(sum, res);
       sample++;
       if (COUNT) c_samples++;
-      if (A.probe_cost) {
-        atomicAdd(A.probe_cost + probe_tile, probe_rounds);
+      if (probe) {
+        probe_end = true;   // its rounds are added to the tile's cost at the top of the next round
         busy = false;
       } else if (sample == A.spp) {
         float *o = A.out + 3 * static_cast<size_t>(pix);

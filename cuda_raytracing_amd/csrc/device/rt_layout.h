@@ -103,6 +103,9 @@ constexpr int kVarNarrow = 1 << 15;
 // run-time compiled scene-specialised kernels of noise scenes: cooperative noise octaves (render_body);
 // the large-scene walks leave it out (its registers cost them a wave; noise is not their bottleneck)
 constexpr int kVarCoop = 1 << 16;
+// run-time compiled kernels: the schedule probe's kernel (kVarProbe) and the render kernels that are never
+// launched as the probe (kVarNoProbe) resolve RenderArgs::probe_cost at compile time (offline: at run time)
+constexpr int kVarProbe = 1 << 17, kVarNoProbe = 1 << 18;
 // variant bits the run-time compiled kernels are specialised on
 constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop |
                             (15 << kVarMatShift) | (15 << kVarTexShift);

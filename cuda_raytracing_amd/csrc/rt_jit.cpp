@@ -82,11 +82,11 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
   const std::string attr = waves_attr();
   *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
          "extern \"C\" __global__ __launch_bounds__(256)" + attr + " void rt_static_render(RenderArgs A) {\n"
-         "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
+         "  render_body<" + std::to_string(v | kVarNoProbe) + ", StaticTrace>(A);\n}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void rt_static_render_count(RenderArgs A) {\n"
-         "  render_body<" + std::to_string(v | kVarCount) + ", StaticTrace>(A);\n}\n"
+         "  render_body<" + std::to_string(v | kVarCount | kVarNoProbe) + ", StaticTrace>(A);\n}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void rt_static_probe(RenderArgs A) {\n"
-         "  render_body<" + std::to_string(v) + ", StaticTrace>(A);\n}\n"
+         "  render_body<" + std::to_string(v | kVarProbe) + ", StaticTrace>(A);\n}\n"
          "}  // namespace rt\n";
   return true;
 }
@@ -308,11 +308,11 @@ std::string jit_lane_source(const SceneImage &img, int variant) {
   const std::string lt = "LaneTraceK<" + std::to_string(scene_kinds(img)) + "u, true>";   // pausable walk
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render(RenderArgs A) {\n  render_body<" +
-         std::to_string(v) + ", " + lt + ">(A);\n}\n";
+         std::to_string(v | kVarNoProbe) + ", " + lt + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_render_count(RenderArgs A) {\n  render_body<" +
-         std::to_string(v | kVarCount) + ", " + lt + ">(A);\n}\n";
+         std::to_string(v | kVarCount | kVarNoProbe) + ", " + lt + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_lane_probe(RenderArgs A) {\n  render_body<" +
-         std::to_string(v) + ", " + lt + ">(A);\n}\n";
+         std::to_string(v | kVarProbe) + ", " + lt + ">(A);\n}\n";
   src += "}  // namespace rt\n";
   return src;
 }
@@ -322,11 +322,11 @@ std::string jit_accel_source(const SceneImage &img, int variant) {
   const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u>";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr() + " void rt_accel_render(RenderArgs A) {\n  render_body<" +
-         std::to_string(v) + ", " + at + ">(A);\n}\n";
+         std::to_string(v | kVarNoProbe) + ", " + at + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render_count(RenderArgs A) {\n  render_body<" +
-         std::to_string(v | kVarCount) + ", " + at + ">(A);\n}\n";
+         std::to_string(v | kVarCount | kVarNoProbe) + ", " + at + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_probe(RenderArgs A) {\n  render_body<" +
-         std::to_string(v) + ", " + at + ">(A);\n}\n";
+         std::to_string(v | kVarProbe) + ", " + at + ">(A);\n}\n";
   src += "}  // namespace rt\n";
   return src;
 }
