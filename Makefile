@@ -24,7 +24,7 @@ ORACLE_FLAGS := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -fopenmp -Wa
 
 HOST_SRC := $(CSRC)/host/rt_host.cpp $(CSRC)/host/image_load.cpp
 HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp \
-            $(CSRC)/sphere_accel.cpp \
+            $(CSRC)/sphere_accel.cpp $(CSRC)/mixed_accel.cpp \
             $(CSRC)/scene_codegen.cpp $(CSRC)/rt_jit.cpp
 HIP_HDR  := $(wildcard $(CSRC)/*.h) $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h \
             $(CSRC)/device/embedded_headers.inc include/rt_render.h include/rt_ref_layout.h

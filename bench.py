@@ -43,7 +43,7 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 import cuda_raytracing_amd as rt  # noqa: E402
 from cuda_raytracing_amd import _abi  # noqa: E402
-from cuda_raytracing_amd.multi_gpu import gather_rows, weak_scaled_resolution  # noqa: E402
+from cuda_raytracing_amd.multi_gpu import gather_rows, max_shard_rows, weak_scaled_resolution  # noqa: E402
 
 # FP32 op weights per event (counted from the reference source, unfused, 1 op each)
 OP_WEIGHTS = {
@@ -57,7 +57,7 @@ OPS_PER_SAMPLE_FIXED = 30                 # camera ray generation
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
-TRAV_NAMES = {0: "lane-dfs", 1: "wave-packet-dfs", 2: "scene-specialised", 3: "verified-sah"}
+TRAV_NAMES = {0: "lane-dfs", 1: "wave-packet-dfs", 2: "scene-specialised", 3: "verified-sah", 4: "verified-mixed"}
 
 
 def log(*a):
@@ -99,15 +99,34 @@ def baseline_oracle():
     return _abi.oracle_lib(), "-O2 -std=c11 -ffp-contract=off -fno-fast-math -fopenmp (prebuilt test build)"
 
 
-def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
-    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample, all cores and 1 core.
+def cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cpu.max quota / period), None if unlimited."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
-    The same sample is then rendered on the GPU through the product context and compared bit for bit
-    (the PSNR half of the BASELINE metric: identical frames -> PSNR = inf, reported as "bit-exact")."""
+
+def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
+    """Oracle (C, OpenMP) on this host: the same scene/camera, a bounded row sample, on EVERY core the
+    process may run on (sched_getaffinity), on the cgroup's CPU quota, and on 1 core.
+
+    BASELINE.md asks for all host cores.  The GPU box exposes 256 hardware threads to the process but its
+    cgroup grants a 16-CPU time quota (cpu.max): a 256-thread run is throttled to that share, so both runs
+    are made and the faster one is the headline (`cores` = its thread count; the other is reported beside
+    it).  `projection_full_host` scales the measured 1-core rate to the machine's physical cores — a
+    projection, not a measurement.  The same sample is then rendered on the GPU through the product context
+    and compared bit for bit (the PSNR half of the BASELINE metric: identical frames -> PSNR = inf)."""
     import ctypes as C
     import numpy as np
     L, build = baseline_oracle()
-    threads = int(L.rt_oracle_threads())
+    default_threads = int(L.rt_oracle_threads())
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or default_threads
+    quota = cpu_quota()
     cam, W, H = rt.camera_from_settings(settings, W, H)
 
     def run(stride, s, offset=0):
@@ -133,18 +152,24 @@ def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
         a = max((t1 - b * n1) / px, 0.0)
         return max(1, math.ceil((a * W * H + b * W * H * spp) / budget))
 
-    # all cores: every stride-th row of the frame at the FULL spp, so the per-pixel work equals the GPU's
-    run(16, 2)
-    stride = sample_stride(budget_s)
-    n, dt, ref = run(stride, spp)
-    rows = ref.shape[0]
-    # one core: a quarter of the budget on a sparser row set (same per-sample work)
-    L.rt_oracle_set_threads(1)
-    try:
-        stride1 = sample_stride(budget_s / 4)
-        n1, dt1, _ = run(stride1, spp, offset=stride1 // 2)
-    finally:
+    def leg(threads, budget, offset=0):
         L.rt_oracle_set_threads(threads)
+        run(16, 2)
+        stride = sample_stride(budget)
+        n, dt, out = run(stride, spp, offset)
+        return {"threads": threads, "value": round(n / dt / 1e6, 3), "stride": stride, "samples": n, "seconds": dt,
+                "out": out}
+
+    legs = []
+    try:
+        legs.append(leg(affinity, budget_s))                       # every core of the affinity mask
+        if quota is not None and int(quota) < affinity:
+            legs.append(leg(max(1, int(quota)), budget_s))          # the cgroup's CPU share
+        one = leg(1, budget_s / 4)
+    finally:
+        L.rt_oracle_set_threads(default_threads)
+    best = max(legs, key=lambda d: d["value"])
+    ref, stride, rows = best["out"], best["stride"], best["out"].shape[0]
     parity = None
     if ctx is not None:
         import torch
@@ -157,16 +182,19 @@ def cpu_baseline(world, settings, W, H, spp, bounces, budget_s, ctx=None):
         parity = {"bit_exact": bool(np.array_equal(g.view(np.uint32), ref.view(np.uint32))),
                   "psnr_db": None if mse == 0 else round(10 * math.log10(1.0 / mse), 2),
                   "note": "GPU vs oracle on this sample; psnr_db null = identical frames (PSNR infinite)"}
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
+    phys = affinity // 2 if affinity >= 2 else 1   # 2 hardware threads per core on the EPYC hosts
     return {
-        "value": round(n / dt / 1e6, 3), "unit": "Msamples/s", "cores": threads, "kind": "port",
-        "sample": f"frame rows 0::{stride} ({rows} rows x {W} px) at spp {spp}, d{bounces}: {n:.3g} samples in {dt:.1f} s",
-        "single_core": {"value": round(n1 / dt1 / 1e6, 3), "unit": "Msamples/s", "cores": 1,
-                        "sample": f"frame rows {stride1 // 2}::{stride1} at spp {spp}: {n1:.3g} samples in {dt1:.1f} s"},
-        "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity,
+        "value": best["value"], "unit": "Msamples/s", "cores": best["threads"], "kind": "port",
+        "sample": f"frame rows 0::{stride} ({rows} rows x {W} px) at spp {spp}, d{bounces}: "
+                  f"{best['samples']:.3g} samples in {best['seconds']:.1f} s on {best['threads']} threads",
+        "legs": [{"threads": d["threads"], "value": d["value"], "sample_rows_stride": d["stride"],
+                  "seconds": round(d["seconds"], 2)} for d in legs],
+        "single_core": {"value": one["value"], "unit": "Msamples/s", "cores": 1,
+                        "sample": f"frame rows 0::{one['stride']} at spp {spp}: {one['samples']:.3g} samples in "
+                                  f"{one['seconds']:.1f} s"},
+        "projection_full_host": {"value": round(one["value"] * phys, 1), "unit": "Msamples/s", "cores": phys,
+                                 "note": "PROJECTION (not measured): 1-core rate x physical cores of the affinity mask"},
+        "cpu_model": cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
         "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "build": build,
         "parity": parity,
     }
@@ -278,6 +306,7 @@ def main():
 
     pending = []
     stats = []
+    gathered = {}   # rank 0: the last frame assembled from every rank's u8 rows
 
     def launch(k, nf):
         i = k % nf
@@ -293,9 +322,11 @@ def main():
         torch.cuda.current_stream().wait_stream(streams[i])
         if world_size > 1:
             if args.dist_backend == "nccl":
-                gather_rows(outs8[i], H, W, rank, world_size)  # u8 rows: 3 B/pixel over xGMI
+                img = gather_rows(outs8[i], H, W, rank, world_size)  # u8 rows: 3 B/pixel over xGMI
             else:
-                gather_rows(outs8[i].cpu(), H, W, rank, world_size)
+                img = gather_rows(outs8[i].cpu(), H, W, rank, world_size)
+            if img is not None:
+                gathered["img"] = img
         stats.append(st)
 
     def run(frames, nf):
@@ -348,6 +379,28 @@ def main():
                      "frames_in_flight": 2, "steps": psteps, "ms_per_step": round(pel / psteps * 1e3, 3),
                      "render_ms_mean": round(sum(st.render_ms for st in pst) / len(pst), 3)}
 
+    # ---- N>1: rank 0 checks the gathered frame (untimed).  The RNG subsequence is the global pixel index, so
+    # its own render of a strided row sample (rows of every rank) must equal those rows of the assembled frame
+    # byte for byte: proof that the shards, the gather and the un-permute put every pixel in place ----
+    dist_check = None
+    if world_size > 1:
+        dist_check = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                      "gather_bytes_per_frame": max_shard_rows(H, world_size) * W * 3 * world_size,
+                      "gather_bit_exact": None}
+        if rank == 0 and "img" in gathered:
+            step = 67 if H > 67 * 4 else max(1, H // 5)   # co-prime with small world sizes: every rank's rows
+            rows_chk = len(range(0, H, step))
+            pchk = rt.make_params(settings, W, H, spp=args.spp, bounces=args.bounces, row_offset=0, row_stride=step,
+                                  row_count=rows_chk)
+            f32 = torch.empty((rows_chk, W, 3), dtype=torch.float32, device="cuda")
+            u8 = torch.empty((rows_chk, W, 3), dtype=torch.uint8, device="cuda")
+            ctx.render_into(cam, pchk, f32.data_ptr(), torch.cuda.current_stream().cuda_stream, u8.data_ptr())
+            ctx.timing()
+            got = gathered["img"][0::step].cpu()
+            dist_check["gather_bit_exact"] = bool(torch.equal(got, u8.cpu()))
+            dist_check["checked_rows"] = f"0::{step} ({rows_chk} rows x {W} px, ranks {sorted({r % world_size for r in range(0, H, step)})})"
+        dist.barrier()
+
     if rank == 0:
         line = {
             "metric": f"Msamples/sec (pixels x spp / s) at {W}x{H} spp={args.spp} d={args.bounces}"
@@ -372,13 +425,15 @@ def main():
                         + (" + gather to rank 0" if world_size > 1 else ""),
                 "pixels_per_gpu": rows * W,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
-                "kernel": {rt.RT_TRAV_STATIC: "rt_static_render (hipRTC)", rt.RT_TRAV_ACCEL: "rt_accel_render (hipRTC)"}.get(
+                "kernel": {rt.RT_TRAV_STATIC: "rt_static_render (hipRTC)", rt.RT_TRAV_ACCEL: "rt_accel_render (hipRTC)",
+                           rt.RT_TRAV_MIXED: "rt_mixed_render (hipRTC)"}.get(
                     cst.traversal, "rt_lane_render (hipRTC)"),
             },
             "kernel_ms": {"render_median": round(render_ms, 3), "seed_median": round(seed_ms, 3),
                           "schedule_median": round(sched_ms, 3),
                           "render_only_msamples_s": round(local_samples / (render_ms / 1e3) / 1e6, 1)},
             "pipelined": pipelined,
+            "distributed": dist_check,
             "roofline": {
                 "bound": "valu",
                 "achieved": round(achieved, 3),

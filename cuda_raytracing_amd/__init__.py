@@ -15,14 +15,14 @@ import numpy as np
 from . import _abi
 from ._abi import (Camera, Params, Scene, Settings, Stats, Vec3, vec3, RT_FLAG_COUNT,
                    RT_FLAG_GLOBAL_SCENE, RT_FLAG_NO_JIT, RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET,
-                   RT_FLAG_FORCE_STATIC, RT_FLAG_NO_FOLD, RT_FLAG_FORCE_ACCEL, RT_FLAG_NO_ACCEL, RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_TRAV_ACCEL, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
+                   RT_FLAG_FORCE_STATIC, RT_FLAG_NO_FOLD, RT_FLAG_FORCE_ACCEL, RT_FLAG_NO_ACCEL, RT_FLAG_RC_AUDIT, RT_FLAG_FORCE_MIXED, RT_FLAG_NO_MIXED, RT_TRAV_MIXED, RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_TRAV_ACCEL, RT_SCENE_COUNT, RT_SCENE_RANDOM_10K, RT_XF_NONE,
                    RT_XF_TRANSLATE, RT_XF_YROTATE, RT_XF_YROTATE_TRANSLATE)
 
 __all__ = [
     "World", "Camera", "Params", "Scene", "Settings", "Stats", "vec3", "build_scene",
     "camera_from_settings", "make_params", "render", "RenderContext", "tonemap", "write_ppm",
     "scene_name", "BlobScene", "shard_rows", "unshard", "RT_FLAG_COUNT", "RT_FLAG_GLOBAL_SCENE",
-    "RT_FLAG_NO_JIT", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_FLAG_FORCE_ACCEL", "RT_FLAG_NO_ACCEL", "RT_TRAV_ACCEL", "RT_TRAV_LANE",
+    "RT_FLAG_NO_JIT", "RT_FLAG_RC_AUDIT", "RT_FLAG_FORCE_MIXED", "RT_FLAG_NO_MIXED", "RT_TRAV_MIXED", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_FLAG_FORCE_ACCEL", "RT_FLAG_NO_ACCEL", "RT_TRAV_ACCEL", "RT_TRAV_LANE",
     "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "accel_build", "tonemap_device", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError", "load_image",
 ]
@@ -325,6 +325,17 @@ def accel_build(scene: Scene):
     buf = np.zeros(total, np.uint32)
     _check(L.rt_accel_build(C.byref(scene), buf.ctypes.data_as(C.c_void_p), total, info), "rt_accel_build")
     return {"root": info[0], "depth": info[1], "spheres": info[2]}, buf[:nw], buf[nw:]
+
+
+def mixed_build(scene: Scene):
+    """Macro roots of the verified mixed-world traversal (no device needed): dict, or None when no
+    transform-free subtree qualifies."""
+    info = (C.c_uint32 * 4)()
+    rc = _abi.hip_lib().rt_mixed_build(C.byref(scene), info)
+    if rc == _abi.RT_ERR_UNSUPPORTED:
+        return None
+    _check(rc, "rt_mixed_build")
+    return {"macros": info[0], "dynamic": info[1], "prims": info[2], "depth": info[3]}
 
 
 def static_compile(scene: Scene, arch: str = "gfx950", max_visits: int = 256) -> str:

@@ -30,7 +30,9 @@ RT_FLAG_NO_JIT = 0x4
 RT_FLAG_FORCE_LANE, RT_FLAG_FORCE_PACKET, RT_FLAG_FORCE_STATIC = 0x8, 0x10, 0x20
 RT_FLAG_NO_FOLD = 0x40
 RT_FLAG_FORCE_ACCEL, RT_FLAG_NO_ACCEL = 0x80, 0x100
-RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_TRAV_ACCEL = 0, 1, 2, 3
+RT_FLAG_RC_AUDIT = 0x200
+RT_FLAG_FORCE_MIXED, RT_FLAG_NO_MIXED = 0x400, 0x800
+RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_TRAV_ACCEL, RT_TRAV_MIXED = 0, 1, 2, 3, 4
 
 CNT_NAMES = [
     "visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate",
@@ -96,6 +98,8 @@ class Stats(C.Structure):
         ("folded", C.c_int32), ("fold_rerenders", C.c_int32),
         ("accel_spheres", C.c_int32), ("accel_depth", C.c_int32),
         ("accel_fallbacks", C.c_uint32), ("jit_source", C.c_int32), ("jit_ms", C.c_double),
+        ("rc_hbm_slots", C.c_uint64), ("rc_lds_levels", C.c_int32), ("mix_macros", C.c_int32),
+        ("mix_fallbacks", C.c_uint32), ("pad_", C.c_int32),
     ]
 
     def counter_dict(self):
@@ -171,7 +175,7 @@ def host_lib():
 HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_render_ppm", "rt_context_timing",
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
-               "rt_seed_states", "rt_kernel_source"]
+               "rt_seed_states", "rt_kernel_source", "rt_mixed_build"]
 
 
 def _bind_single_hip_runtime():
@@ -215,6 +219,7 @@ def hip_lib():
         _sig(L.rt_context_note, C.c_char_p, P)
         _sig(L.rt_tonemap_device, C.c_int, P, C.c_uint64, P, P)
         _sig(L.rt_accel_build, C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
+        _sig(L.rt_mixed_build, C.c_int, C.POINTER(Scene), C.POINTER(C.c_uint32))
         _sig(L.rt_seed_states, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_kernel_source, C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.c_char_p, C.c_uint64)
         _hip = L

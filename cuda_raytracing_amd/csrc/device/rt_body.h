@@ -978,6 +978,292 @@ struct AccelTraceK {
 };
 
 // ---------------------------------------------------------------------------------------------
+// traversal policy 5: verified traversal of mixed worlds (mixed_accel.cpp)
+// ---------------------------------------------------------------------------------------------
+// The reference's own DFS (LaneTrace) above the macro roots — transforms, their in-place ray drift and
+// the visit order included — and, at a macro root whose box test passes (W_MACRO), one SAH walk over its
+// transform-free primitives instead of the reference's walk of that subtree.  Inside a macro the ray is
+// never modified (static macro: no transform below; dynamic macro: entered only when the reference's
+// slab test on W_XFBOX, the union of the boxes of the BVH nodes with a transform child below, fails —
+// those nodes then fail too at their visit: smaller box, smaller tmax, same ray, and the rounded slab
+// values are monotone in the bounds for finite 1/dir).  So the subtree's effect on the record is that of
+// its closest acceptable primitive the reference reaches, unless two candidates tie.  Per primitive the
+// candidate value v does not depend on tmax (sphere: the root hit() would accept for any tmax > v;
+// quad / triangle: the plane t when the point is inside), and the reference accepts it iff v < tmax
+// (sphere) or v <= tmax (quad, triangle: :1066).  The walk keeps
+//   best    the smallest v below min(best, tmax_in), with its deepest reference BVH ancestor A below the
+//           macro root (its "group": every primitive under that node shares it),
+//   tie     some candidate equal to min(best, tmax_in) (the reference's order would decide),
+//   second  a lower bound on v over the primitives outside best's group (pruning bound included),
+// and proves reach: the reference visits A with the tmax of that moment, T_A = min(tmax_in, v of the
+// primitives it accepted before A), all outside A's subtree, so T_A >= lb = min(tmax_in, second, bound);
+// the reference's own slab test of A with tmax = lb passing implies it passes at T_A, and then every
+// ancestor of A passes too (their boxes contain A's, their tmax is larger).  A ray that fails a check
+// (tie, reach, or a non-finite / unbounded ray) takes the reference's walk of that subtree instead.
+// Culling is conservative as in AccelTraceK (boxes padded by kAccelKappa (M + |o|_1)); the pruning bound
+// exceeds best by 2^-16 best so that the reach test's near-boundary cases (a box face hit, where A's
+// entry slab value and the plane t are two roundings of one number) see every competitor.
+constexpr float kMixBoundRel = 1.52587890625e-05f;   // 2^-16
+
+__device__ __forceinline__ bool mix_box(const Trav &T, const SlabRay &R, float x0, float x1, float y0, float y1, float z0,
+                                        float z1, float bound, float *tnear) {
+  const float nx = __builtin_fmaf(R.nx ? x1 : x0, T.inv.x, R.on.x), fx = __builtin_fmaf(R.nx ? x0 : x1, T.inv.x, R.of.x);
+  const float ny = __builtin_fmaf(R.ny ? y1 : y0, T.inv.y, R.on.y), fy = __builtin_fmaf(R.ny ? y0 : y1, T.inv.y, R.of.y);
+  const float nz = __builtin_fmaf(R.nz ? z1 : z0, T.inv.z, R.on.z), fz = __builtin_fmaf(R.nz ? z0 : z1, T.inv.z, R.of.z);
+  const float t0 = fmaxf(fmaxf(nx, ny), fmaxf(nz, kTmin)), t1 = fminf(fminf(fx, fy), fminf(fz, bound));
+  *tnear = t0;
+  return !(t1 < t0);
+}
+
+// candidate value of a quad / triangle (geom_calc_hit, :1060-1077, + the inside test of :1131-1175): the
+// plane t when t >= tmin and the point is inside; ok = false otherwise.  Same operations as planar_hit.
+__device__ __forceinline__ float planar_value(const Ray &r, bool tri, f3 n, float dd, f3 q, f3 uu, f3 vv, f3 ww, bool &ok) {
+  ok = false;
+  float t = 0.0f;
+  const float denom = dot(n, r.d);
+  if (fabsf(denom) >= kDenomEps) {
+    t = (dd - dot(n, r.o)) / denom;
+    if (kTmin <= t) {
+      const f3 p = line_at(r.o, t, r.d);
+      const f3 pq = sub(p, q);
+      const float alpha = dot(ww, cross(pq, vv));
+      const float beta = dot(ww, cross(uu, pq));
+      bool inside = (0.0f <= alpha) & (alpha <= 1.0f) & (0.0f <= beta) & (beta <= 1.0f);
+      if (tri) inside = inside & (alpha + beta <= 1.0f);
+      ok = inside;
+    }
+  }
+  return t;
+}
+
+// candidate value of a sphere (:1093-1110): the root hit() accepts for any tmax above it
+__device__ __forceinline__ float sphere_value(const Ray &r, f3 c0, f3 mv, float rad2, bool &ok) {
+  const f3 center = line_at(c0, r.time, mv);
+  const f3 oc = sub(center, r.o);
+  const float a = dot(r.d, r.d);
+  const float b = -2.0f * dot(r.d, oc);
+  const float c = dot(oc, oc) - rad2;
+  const float disc = b * b - 4 * a * c;
+  ok = false;
+  if (!(disc >= 0)) return 0.0f;
+  const float sq = sqrtf(disc);
+  float root = (-b - sq) / (2.0f * a);
+  if (kTmin >= root || root >= __builtin_huge_valf()) root = (-b + sq) / (2.0f * a);
+  ok = kTmin < root && root < __builtin_huge_valf();
+  return root;
+}
+
+template <uint32_t KM>
+struct MixedTraceK {
+  template <bool LDS, bool COUNT, bool UV>
+  __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t lanes,
+                                             uint32_t lane, uint16_t *stk, Trav &T, Ray &r, Hit &h, Visits &vc) {
+    if (COUNT) {   // the counting variant walks the reference tree (the op model counts its visits)
+      LaneTraceK<KM, false, true>::template run<LDS, COUNT, UV>(S, A, busy, lanes, lane, stk, T, r, h, vc);
+      return;
+    }
+    if (!busy) return;
+    trav_reset(T, r);
+    stk[0] = static_cast<uint16_t>(A.root);
+    T.sp = 1;
+    T.active = 0;
+    const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.mix_nodes);
+    const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.mix_prims);
+    bool walking = true, in_macro = false;
+    uint32_t mroot = 0, mnode = 0, bprim = 0, bgroup = 0;
+    int msp = 0;
+    float tin = 0.0f, best = __builtin_huge_valf(), second = __builtin_huge_valf();
+    bool tie = false;
+    SlabRay sr;
+    sr.on = mk(0, 0, 0); sr.of = mk(0, 0, 0); sr.nx = sr.ny = sr.nz = false;
+    while (__ballot(walking) != 0) {
+      if (!walking) continue;
+      if (!in_macro) {
+        if (T.sp == 0) { walking = false; continue; }
+        // ---- one step of the reference walk (trav_step), macro roots aside ----
+        int sp = T.sp - 1;
+        const uint32_t idx = stk[sp * 64];
+        const uint32_t nb = idx * kNodeWords;
+        const uint4 w0 = S.w4(nb), w1 = S.w4(nb + 4), w2 = S.w4(nb + 8), w3 = S.w4(nb + 12), w4 = S.w4(nb + 16);
+        const uint32_t kind = w0.x;
+        const bool in_xf = T.tc || T.yc;
+        bool expand = false;   // a BVH node whose box passed / a group: push its children (unless a macro)
+        if ((KM & (1u << K_BVH)) && kind == K_BVH) {
+          expand = box_hit(T, r, asf(w0.z), asf(w0.w), asf(w1.x), asf(w1.y), asf(w1.z), asf(w1.w));
+        } else if ((KM & (1u << K_GROUP)) && kind == K_GROUP) {
+          expand = true;
+        } else if ((KM & ((1u << K_QUAD) | (1u << K_TRIANGLE))) && (kind == K_QUAD || kind == K_TRIANGLE)) {
+          planar_hit(T, r, h, kind == K_TRIANGLE, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), asf(w1.y),
+                     mk(asf(w1.z), asf(w1.w), asf(w2.x)), mk(asf(w2.y), asf(w2.z), asf(w2.w)),
+                     mk(asf(w3.x), asf(w3.y), asf(w3.z)), mk(asf(w3.w), asf(w4.x), asf(w4.y)), in_xf);
+        } else if ((KM & (1u << K_SPHERE)) && kind == K_SPHERE) {
+          sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
+                         asf(w2.y), asf(w2.z), in_xf);
+        } else if ((KM & (1u << K_TRANSLATE)) && kind == K_TRANSLATE) {
+          const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
+          if (T.tc == 0) {
+            translate_enter(T, r, off);
+            stk[sp * 64] = static_cast<uint16_t>(idx);
+            stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+            sp += 2;
+            T.tc++;
+          } else {
+            T.tc--;
+            translate_exit(T, r, h, off);
+          }
+        } else if ((KM & (1u << K_YROTATE)) && kind == K_YROTATE) {
+          if (T.yc == 0) {
+            rotate_enter(T, r, asf(w0.z), asf(w0.w));
+            stk[sp * 64] = static_cast<uint16_t>(idx);
+            stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+            sp += 2;
+            T.yc++;
+          } else {
+            T.yc--;
+            rotate_exit(T, r, h, asf(w0.z), asf(w0.w));
+          }
+        }
+        if (expand) {
+          const uint32_t mw = w3.x;   // W_MACRO
+          bool macro = mw != 0;
+          if (macro) {
+            // bounded, finite rays only (finite 1/dir: the slab arithmetic stays monotone, the conservative
+            // boxes hold); a dynamic macro only when the ray misses W_XFBOX in the reference's own test
+            const float ao = fabsf(r.o.x) + fabsf(r.o.y) + fabsf(r.o.z);
+            const float dmin = fminf(fminf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+            const float dmax = fmaxf(fmaxf(fabsf(r.d.x), fabsf(r.d.y)), fabsf(r.d.z));
+            macro = (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f);
+            if (macro && (mw & kMacroDynamic))
+              macro = !box_hit(T, r, asf(w3.y), asf(w3.z), asf(w3.w), asf(w4.x), asf(w4.y), asf(w4.z));
+            if (macro) {
+              in_macro = true;
+              mroot = idx;
+              mnode = mw & kMacroRootMask;
+              msp = 0;
+              tin = T.tmax;
+              best = __builtin_huge_valf();
+              second = __builtin_huge_valf();
+              bprim = 0; bgroup = kMixNoGroup;
+              tie = false;
+              const float pad_o = kAccelKappa * ao;
+              const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
+              const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
+              sr = slab_ray(T, oinv, pinv);
+            }
+          }
+          if (!macro) {
+            if (kind == K_BVH) {
+              stk[sp * 64] = static_cast<uint16_t>(w0.y >> 16);      // right
+              stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);      // left (popped first)
+              sp += 2;
+            } else {
+              const uint32_t first = w0.y, n = w0.z;
+              for (uint32_t i = 0; i < n; ++i) stk[(sp + i) * 64] = static_cast<uint16_t>(first + i);
+              sp += n;
+            }
+          }
+        }
+        T.sp = sp;
+        continue;
+      }
+      // ---- one step of the macro's SAH walk ----
+      const float cur = fminf(best, tin);
+      const float bound = best < __builtin_huge_valf() ? fminf(tin, best + best * kMixBoundRel) : tin;
+      const uint4 q0 = N[mnode * 4], q1 = N[mnode * 4 + 1], q2 = N[mnode * 4 + 2], q3 = N[mnode * 4 + 3];
+      float n0, n1;
+      bool h0 = mix_box(T, sr, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), bound, &n0);
+      bool h1 = mix_box(T, sr, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w), bound, &n1);
+      const bool near0 = n0 <= n1;
+      const uint32_t rn = near0 ? q3.x : q3.y, rf = near0 ? q3.y : q3.x;
+      bool hn = near0 ? h0 : h1, hf = near0 ? h1 : h0;
+      const bool ln = hn && (rn & kAccelLeaf), lf = hf && (rf & kAccelLeaf);
+      const uint32_t c1 = ln ? ((rn >> 24) & 0x7fu) + 1u : 0u, c2 = lf ? ((rf >> 24) & 0x7fu) + 1u : 0u;
+      const uint32_t f1 = rn & 0xffffffu, f2 = (rf & 0xffffffu) - c1;
+      float cur_k = cur;
+      for (uint32_t k = 0; k < c1 + c2; ++k) {
+        const uint32_t pr = (k < c1 ? f1 : f2) + k;
+        const uint4 *pw = P + static_cast<size_t>(pr) * (kMixPrimWords / 4);
+        const uint4 p0 = pw[0], p1 = pw[1], p2 = pw[2];
+        bool ok;
+        float v;
+        if ((KM & (1u << K_SPHERE)) && p0.x == K_SPHERE) {
+          v = sphere_value(r, mk(asf(p0.z), asf(p0.w), asf(p1.x)), mk(asf(p1.y), asf(p1.z), asf(p1.w)), asf(p2.y), ok);
+        } else {
+          const uint4 p3 = pw[3], p4 = pw[4];
+          v = planar_value(r, p0.x == K_TRIANGLE, mk(asf(p0.z), asf(p0.w), asf(p1.x)), asf(p1.y),
+                           mk(asf(p1.z), asf(p1.w), asf(p2.x)), mk(asf(p2.y), asf(p2.z), asf(p2.w)),
+                           mk(asf(p3.x), asf(p3.y), asf(p3.z)), mk(asf(p3.w), asf(p4.x), asf(p4.y)), ok);
+        }
+        if (ok) {
+          const uint32_t g = pw[5].x;   // MP_GROUP
+          if (v < cur_k) {
+            if (best < __builtin_huge_valf() && g != bgroup) second = fminf(second, best);
+            best = v; bprim = pr; bgroup = g;
+            cur_k = v;
+          } else if (v == cur_k) {
+            tie = true;
+          } else if (g != bgroup) {
+            second = fminf(second, v);
+          }
+        }
+      }
+      hn = hn && !ln;
+      hf = hf && !lf;
+      if (hn && hf) {
+        stk[(T.sp + msp) * 64] = static_cast<uint16_t>(rf);
+        ++msp;
+        mnode = rn;
+        continue;
+      }
+      if (hn | hf) { mnode = hn ? rn : rf; continue; }
+      if (msp > 0) { --msp; mnode = stk[(T.sp + msp) * 64]; continue; }
+      // ---- walk done: prove the record, commit it, or hand the subtree to the reference walk ----
+      in_macro = false;
+      bool ok = !tie && !A.mix_no_proof;
+      const uint4 *bw = P + static_cast<size_t>(bprim) * (kMixPrimWords / 4);
+      if (ok && best < __builtin_huge_valf() && bgroup != kMixNoGroup) {
+        const float bnd = fminf(tin, best + best * kMixBoundRel);
+        const uint4 g0 = bw[5], g1 = bw[6];
+        Trav tt = T;
+        tt.tmax = fminf(fminf(tin, second), bnd);
+        ok = box_hit(tt, r, asf(g0.y), asf(g0.z), asf(g0.w), asf(g1.x), asf(g1.y), asf(g1.z));
+      }
+      if (ok) {
+        if (best < __builtin_huge_valf()) {
+          const uint4 p0 = bw[0], p1 = bw[1], p2 = bw[2], p3 = bw[3], p4 = bw[4];
+          if ((KM & (1u << K_SPHERE)) && p0.x == K_SPHERE) {
+            T.tmax = best;
+            sphere_commit<UV>(T, r, h, p0.y, mk(asf(p0.z), asf(p0.w), asf(p1.x)), mk(asf(p1.y), asf(p1.z), asf(p1.w)), asf(p2.z));
+          } else {
+            // planar_hit's record at t = best (tmax = best: the same plane test accepts it)
+            T.tmax = best;
+            planar_hit(T, r, h, p0.x == K_TRIANGLE, p0.y, mk(asf(p0.z), asf(p0.w), asf(p1.x)), asf(p1.y),
+                       mk(asf(p1.z), asf(p1.w), asf(p2.x)), mk(asf(p2.y), asf(p2.z), asf(p2.w)),
+                       mk(asf(p3.x), asf(p3.y), asf(p3.z)), mk(asf(p3.w), asf(p4.x), asf(p4.y)), false);
+          }
+          T.result = true;
+          if (T.tc || T.yc) T.was_last = 1;
+        }
+      } else {   // the reference's own expansion of the macro root (its box test already passed)
+        if (A.mix_fallbacks) atomicAdd(A.mix_fallbacks, 1u);   // rare (diagnostic)
+        const uint32_t nb = mroot * kNodeWords;
+        const uint4 w0 = S.w4(nb);
+        int sp = T.sp;
+        if (w0.x == K_BVH) {
+          stk[sp * 64] = static_cast<uint16_t>(w0.y >> 16);
+          stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+          sp += 2;
+        } else {
+          for (uint32_t i = 0; i < w0.z; ++i) stk[(sp + i) * 64] = static_cast<uint16_t>(w0.y + i);
+          sp += w0.z;
+        }
+        T.sp = sp;
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
 // traversal policy 2: one DFS per wave with per-entry lane masks
 // ---------------------------------------------------------------------------------------------
 // The reference's DFS order is fixed by the scene, not by the ray: a hit BVH node pushes right then

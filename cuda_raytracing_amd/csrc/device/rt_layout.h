@@ -39,6 +39,21 @@ constexpr uint32_t kAccelLeaf = 0x80000000u;
 constexpr float kAccelKappa = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24): cone padding per unit of |oc|
 enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
 
+// Verified traversal of mixed worlds (mixed_accel.cpp, MixedTraceK): some reference BVH/group nodes are
+// macro roots, whose transform-free primitives (quads, triangles, spheres) also sit in a SAH tree of their
+// own (node layout as above).  Node words W_MACRO (the SAH root | kMacro* flags, 0 = plain node) and
+// W_XFBOX..+5 (dynamic macros: the union of the boxes of the BVH nodes below with a translate / rotate
+// child) are unused by the record kinds (a BVH node ends at word 7, a group at word 2).  Static macro:
+// the subtree holds no transform.  Dynamic macro: the ray may take the SAH walk only when the reference's
+// own slab test on W_XFBOX fails (then it enters no transform below).
+constexpr int W_MACRO = 12, W_XFBOX = 13;
+constexpr uint32_t kMacroStatic = 0x80000000u, kMacroDynamic = 0x40000000u, kMacroRootMask = 0x00ffffffu;
+// Mixed prims (leaf order): words 0..19 = the primitive's node record (kind, material, geometry), MP_GROUP =
+// its deepest reference BVH ancestor below the macro root (~0u: none), MP_GBOX..+5 = that ancestor's box
+constexpr int kMixPrimWords = 32;
+enum : int { MP_GROUP = 20, MP_GBOX = 21, MP_RECORD = 27 };
+constexpr uint32_t kMixNoGroup = 0xffffffffu;
+
 // materials (raytracing.cu:78-99): 8 words; kinds == RTR_MAT_* (rt_ref_layout.h).  A metal's albedo
 // sits at words 1..3 like a solid texture's colour (M_TEX is only used by Lambertian / light kinds), so
 // both are "colour records" the compact colour stack can point at (see kRecWords below).
@@ -174,6 +189,9 @@ struct RenderArgs {
                                   // (0,0,0) unwinds to +0 without reading its colour stack
   uint32_t coop_noise;            // noise kernels: spread perlin_turbulence's octaves over the wave's lanes
                                   // when at most this many (<= 32) lanes need one (0 = never)
+  uint32_t mix_nodes, mix_prims;  // verified mixed-world traversal: word offsets of its SAH nodes / prims
+  uint32_t *mix_fallbacks;        // macro walks it handed back to the reference walk (diagnostic)
+  uint32_t mix_no_proof;          // test aid (RT_MIX_PROVE=0): every macro walk takes the fallback
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

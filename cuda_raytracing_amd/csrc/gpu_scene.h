@@ -35,6 +35,15 @@ struct SphereAccel {
 // false (with a reason) when the world is not an all-sphere BVH/group tree with >= min_spheres spheres
 bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel *out, std::string *why);
 
+// Verified traversal of mixed worlds (mixed_accel.cpp): SAH trees of the macro roots' transform-free
+// primitives.  build_mixed_accel also writes W_MACRO / W_XFBOX into `img`'s node words.
+struct MixedAccel {
+  std::vector<uint32_t> node_words, prim_words;
+  uint32_t macros = 0, dynamic = 0, prims = 0, depth = 0;
+};
+// false (with a reason) when no node qualifies (e.g. a world of transforms only)
+bool build_mixed_accel(SceneImage *img, MixedAccel *out, std::string *why);
+
 // Returns RT_OK or RT_ERR_SCENE / RT_ERR_UNSUPPORTED.
 int compile_scene(const void *scene /* const rt_scene* */, SceneImage *out);
 

@@ -143,6 +143,11 @@ struct rt_context {
   rt::SphereAccel accel;
   bool accel_ok = false;
   uint32_t accel_nodes = 0, accel_prims = 0;   // word offsets in the device image
+  // verified mixed-world traversal (RT_TRAV_MIXED): macro roots marked in the image, SAH words appended
+  rt::MixedAccel mixed;
+  bool mixed_ok = false;
+  uint32_t mix_nodes = 0, mix_prims = 0;
+  bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
   DevBuf scene, jump, rng, rc, work, counters, wave_trace, tile_cost, tile_order;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
@@ -186,6 +191,9 @@ struct rt_context {
   bool rendered = false;
   uint64_t samples = 0;
   size_t lds_bytes = 0;
+  size_t rc_audit_bytes = 0;      // RT_FLAG_RC_AUDIT: bytes of the HBM colour-stack buffer filled before the render
+  bool rc_audit_narrow = false;   // ... holding 16-bit codes
+  uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
   double jit_ms = 0.0;            // ... and the host time spent obtaining them
 };
@@ -212,6 +220,21 @@ int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_
     std::memcpy(words, a.node_words.data(), a.node_words.size() * 4);
     std::memcpy(words + a.node_words.size(), a.prim_words.data(), a.prim_words.size() * 4);
   }
+  return RT_OK;
+}
+
+int rt_mixed_build(const rt_scene *scene, uint32_t info[4]) {
+  if (!scene || !info) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  int st = rt::compile_scene(scene, &img);
+  if (st != RT_OK) return st;
+  rt::MixedAccel m;
+  std::string why;
+  if (!rt::build_mixed_accel(&img, &m, &why)) return RT_ERR_UNSUPPORTED;
+  info[0] = m.macros;
+  info[1] = m.dynamic;
+  info[2] = m.prims;
+  info[3] = m.depth;
   return RT_OK;
 }
 
@@ -281,20 +304,31 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_DEFER_TRACE")) c->defer_trace = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+  if (const char *e = std::getenv("RT_MIX_PROVE")) c->mix_no_proof = e[0] == '0';
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
-  std::vector<uint32_t> dev_words = c->img.words;
   {
     const char *e = std::getenv("RT_ACCEL");
     std::string why;
-    if (!(e && e[0] == '0') && rt::build_sphere_accel(c->img, kAccelMinSpheres, &c->accel, &why)) {
-      c->accel_ok = true;
-      c->accel_nodes = static_cast<uint32_t>(dev_words.size());
-      dev_words.insert(dev_words.end(), c->accel.node_words.begin(), c->accel.node_words.end());
-      c->accel_prims = static_cast<uint32_t>(dev_words.size());
-      dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
-    }
+    if (!(e && e[0] == '0') && rt::build_sphere_accel(c->img, kAccelMinSpheres, &c->accel, &why)) c->accel_ok = true;
+    // worlds the sphere walk cannot take: macro roots for the mixed walk (marks W_MACRO / W_XFBOX in the
+    // node words, which every other traversal ignores)
+    const char *m = std::getenv("RT_MIXED");
+    if (!c->accel_ok && !(m && m[0] == '0') && rt::build_mixed_accel(&c->img, &c->mixed, &why)) c->mixed_ok = true;
+  }
+  std::vector<uint32_t> dev_words = c->img.words;
+  if (c->accel_ok) {
+    c->accel_nodes = static_cast<uint32_t>(dev_words.size());
+    dev_words.insert(dev_words.end(), c->accel.node_words.begin(), c->accel.node_words.end());
+    c->accel_prims = static_cast<uint32_t>(dev_words.size());
+    dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
+  }
+  if (c->mixed_ok) {
+    c->mix_nodes = static_cast<uint32_t>(dev_words.size());
+    dev_words.insert(dev_words.end(), c->mixed.node_words.begin(), c->mixed.node_words.end());
+    c->mix_prims = static_cast<uint32_t>(dev_words.size());
+    dev_words.insert(dev_words.end(), c->mixed.prim_words.begin(), c->mixed.prim_words.end());
   }
   // per-lane u16 stacks of 4 waves x 64 lanes: 512 B per entry; 256 entries (128 KiB) plus the minimum
   // colour-stack levels is what one 160 KiB block can hold (checked again per render)
@@ -373,7 +407,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
   size_t rc_bytes = rc_levels * rc_level_bytes(false);
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
-  const uint32_t stack_cap = std::max(c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u);
+  // (the mixed walk keeps a macro's SAH stack above the reference walk's entries)
+  const uint32_t stack_cap = std::max({c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u,
+                                       c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u});
   size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
   // one block may declare at most the CU's 160 KiB: a deep per-lane stack first evicts the LDS copy of
   // the scene (read from HBM instead); if the stack and the minimum colour-stack levels alone do not
@@ -398,9 +434,13 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   else if (p->flags & RT_FLAG_FORCE_PACKET) trav = RT_TRAV_PACKET;
   else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
   else if (p->flags & RT_FLAG_FORCE_ACCEL) trav = RT_TRAV_ACCEL;
-  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC || trav == RT_TRAV_ACCEL)) trav = RT_TRAV_LANE;
+  else if (p->flags & RT_FLAG_FORCE_MIXED) trav = RT_TRAV_MIXED;
+  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC || trav == RT_TRAV_ACCEL || trav == RT_TRAV_MIXED))
+    trav = RT_TRAV_LANE;
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
-  if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = RT_TRAV_LANE;
+  const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
+  if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;
+  if (trav == RT_TRAV_MIXED && !mixed_allowed) trav = RT_TRAV_LANE;
   if (trav == RT_TRAV_PACKET && c->img.stack_need > 64) trav = RT_TRAV_LANE;
   hipFunction_t jit_fn = nullptr, jit_probe = nullptr;
   bool jit_lane = false;
@@ -426,7 +466,20 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
       trav = RT_TRAV_STATIC;
     } else {
       c->jit_why = why;
-      trav = accel_allowed ? RT_TRAV_ACCEL : RT_TRAV_LANE;
+      trav = accel_allowed ? RT_TRAV_ACCEL : (mixed_allowed ? RT_TRAV_MIXED : RT_TRAV_LANE);
+    }
+  }
+  if (trav == RT_TRAV_MIXED) {
+    rt::JitKernels jk;
+    std::string why;
+    if (rt::jit_mixed_kernels(c->img, c->variant | trace_bit, &jk, &why)) {
+      note_jit(jk);
+      jit_fn = c->counted ? jk.render_count : jk.render;
+      jit_probe = jk.probe;
+      jit_lane = true;   // per-lane stacks
+    } else {
+      c->jit_why = why;
+      trav = RT_TRAV_LANE;
     }
   }
   if (trav == RT_TRAV_ACCEL) {
@@ -501,6 +554,13 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const uint32_t n_ids = 64u * ((static_cast<uint32_t>(p->row_count) + 7) / 8) * tiles_x;
   if (c->rng.ensure(static_cast<size_t>(n_ids) * 6 * 4) != hipSuccess) return RT_ERR_HIP;
   if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;
+  c->used_rc_levels = rc_levels;
+  c->rc_audit_bytes = 0;
+  if (p->flags & RT_FLAG_RC_AUDIT) {   // every slot 0xff..: a written code never is (rt_layout.h kRc*)
+    c->rc_audit_bytes = static_cast<size_t>(mb) * threads * (narrow ? 2 : 4);
+    c->rc_audit_narrow = narrow;
+    if (hipMemsetAsync(c->rc.p, 0xff, c->rc_audit_bytes, s) != hipSuccess) return RT_ERR_HIP;
+  }
 
   rt::SeedArgs sa{};
   sa.jump = static_cast<const uint32_t *>(c->jump.p);
@@ -523,6 +583,10 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.accel_prims = c->accel_prims;
   a.accel_root = c->accel.root;
   a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
+  a.mix_nodes = c->mix_nodes;
+  a.mix_prims = c->mix_prims;
+  a.mix_fallbacks = static_cast<uint32_t *>(c->work.p) + 11;
+  a.mix_no_proof = c->mix_no_proof ? 1u : 0u;
   a.rc_lds_word = scene_lds_words;
   a.rc_lds_levels = rc_levels;
   a.rc_tex0 = c->img.mat_count;
@@ -595,6 +659,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     pa.wave_trace = nullptr;
     pa.fold_violation = static_cast<uint32_t *>(c->work.p) + 14;   // probe rays: flag ignored
     pa.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 13;  // probe rays: not reported
+    pa.mix_fallbacks = static_cast<uint32_t *>(c->work.p) + 10;
     const hipError_t pe = jit_probe ? rt::jit_launch(jit_probe, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                     : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
                                                         c->lds_bytes, s);
@@ -637,7 +702,9 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->fold_rerenders = static_cast<int32_t>(c->fold_violations);
   st->accel_spheres = c->accel_ok ? static_cast<int32_t>(c->accel.spheres) : 0;
   st->accel_depth = c->accel_ok ? static_cast<int32_t>(c->accel.depth) : 0;
+  st->mix_macros = c->mixed_ok ? static_cast<int32_t>(c->mixed.macros) : 0;
   if (!c->rendered) return RT_OK;
+  st->rc_lds_levels = static_cast<int32_t>(c->used_rc_levels);
   st->jit_source = c->jit_source;
   st->jit_ms = c->jit_ms;
   DeviceGuard g(c->device);
@@ -663,10 +730,25 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   if (c->used_traversal == RT_TRAV_ACCEL &&
       hipMemcpy(&st->accel_fallbacks, static_cast<uint32_t *>(c->work.p) + 12, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return RT_ERR_HIP;
+  if (c->used_traversal == RT_TRAV_MIXED &&
+      hipMemcpy(&st->mix_fallbacks, static_cast<uint32_t *>(c->work.p) + 11, 4, hipMemcpyDeviceToHost) != hipSuccess)
+    return RT_ERR_HIP;
   st->init_ms = a;
   st->sched_ms = b;
   st->render_ms = d;
   st->samples = c->samples;
+  if (c->rc_audit_bytes) {   // RT_FLAG_RC_AUDIT: slots the render wrote
+    std::vector<uint8_t> rb(c->rc_audit_bytes);
+    if (hipMemcpy(rb.data(), c->rc.p, rb.size(), hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
+    const size_t w = c->rc_audit_narrow ? 2 : 4;
+    uint64_t n = 0;
+    for (size_t i = 0; i < rb.size(); i += w) {
+      bool untouched = true;
+      for (size_t k = 0; k < w; ++k) untouched = untouched && rb[i + k] == 0xff;
+      n += untouched ? 0 : 1;
+    }
+    st->rc_hbm_slots = n;
+  }
   if (c->counted) {
     unsigned long long h[RT_CNT__COUNT];
     if (hipMemcpy(h, c->counters.p, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
@@ -774,6 +856,11 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     std::string why;
     if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
     src = rt::jit_accel_source(img, variant);
+  } else if (traversal == RT_TRAV_MIXED) {
+    rt::MixedAccel m;
+    std::string why;
+    if (!rt::build_mixed_accel(&img, &m, &why)) return RT_ERR_UNSUPPORTED;
+    src = rt::jit_mixed_source(img, variant);
   } else if (traversal == RT_TRAV_LANE) {
     src = rt::jit_lane_source(img, variant);
   } else {

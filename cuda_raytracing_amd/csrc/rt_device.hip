@@ -58,10 +58,14 @@ __device__ __forceinline__ void jump_next(const uint4 *__restrict__ lo, const ui
   x0 = r0; x1 = r1; x2 = r2; x3 = r3; x4 = r4;
 }
 
-// Thread t seeds a run of kSeedRun consecutive pixels of one row (one jump, then P_0 steps).  Threads
-// are ordered (8-row band, run, row in band): the 8 rows of a run are consecutive lanes, so each store
-// step of a wave fills whole 32-B row segments of 8x8 tiles in the tile-major state layout
-// (RenderArgs::rng) — the render then reads a tile's 64 states as 256 contiguous bytes per word.
+// Thread t seeds a run of kSeedRun = 16 consecutive pixels of one row (one jump, then P_0 steps): the
+// row segments of two horizontally adjacent 8x8 tiles.  Threads are ordered (8-row band, run, row in
+// band), so the 8 rows of a run are consecutive lanes.  The 16 states stay in registers until the run is
+// done; then each lane stores its two 32-B tile-row segments per state word as 16-B vector stores, and
+// the 8 lanes of a run together write each tile's 256 contiguous bytes (two whole 128-B lines) in one
+// store instruction.  (Storing each state as it was produced wrote one 4-B piece into 16 different
+// lines per instruction: 3.3x the states' bytes reached HBM, profiles/r02_v8_traffic.)  Columns past the
+// frame edge inside the last tile are written too (never read).
 __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
   __shared__ uint4 s_lo[kJumpNibbles * 16];
   __shared__ uint32_t s_hi[kJumpNibbles * 16];
@@ -71,13 +75,13 @@ __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
     for (uint32_t i = threadIdx.x; i < kJumpNibbles * 16; i += kBlock) { s_lo[i] = glo[i]; s_hi[i] = ghi[i]; }
     __syncthreads();
   }
+  static_assert(kSeedRun == 16, "a run is two tile rows");
   const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t W = static_cast<uint32_t>(A.width);
   const uint32_t runs = (W + kSeedRun - 1) / kSeedRun;
   const uint32_t band = t / (8u * runs), q = t - band * 8u * runs;
   const uint32_t lr = band * 8u + (q & 7u), j0 = (q >> 3) * kSeedRun;
   if (lr >= A.rows) return;
-  const uint32_t j1 = min(j0 + kSeedRun, W);
   uint32_t x0 = A.base[1], x1 = A.base[2], x2 = A.base[3], x3 = A.base[4], x4 = A.base[5];
   {
     const uint64_t g = static_cast<uint64_t>(A.row_offset + static_cast<int64_t>(lr) * A.row_stride) * W + j0;
@@ -86,12 +90,26 @@ __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
       if ((g >> k) & 1u) jump_apply(A.jump + k * kJumpMatrixWords, x0, x1, x2, x3, x4);
   }
   const uint32_t n = A.n_ids;
-  const uint32_t row_base = (lr >> 3) * A.tiles_x * 64u + (lr & 7u) * 8u;
-  for (uint32_t j = j0; j < j1; ++j) {
-    if (j > j0) jump_next(s_lo, s_hi, x0, x1, x2, x3, x4);     // P_0: next global pixel in the row
-    const uint32_t id = row_base + (j >> 3) * 64u + (j & 7u);
-    A.rng[id] = A.base[0];
-    A.rng[n + id] = x0; A.rng[2 * n + id] = x1; A.rng[3 * n + id] = x2; A.rng[4 * n + id] = x3; A.rng[5 * n + id] = x4;
+  const uint32_t id0 = (lr >> 3) * A.tiles_x * 64u + (j0 >> 3) * 64u + (lr & 7u) * 8u;   // tile A, this row
+  const bool second = (j0 >> 3) + 1u < A.tiles_x;                                          // tile B exists
+  const uint4 d = make_uint4(A.base[0], A.base[0], A.base[0], A.base[0]);
+  for (int h = 0; h < 2; ++h) {   // tile A's row segment, then tile B's
+    if (h == 1 && !second) break;
+    uint32_t st[5][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (h + j > 0) jump_next(s_lo, s_hi, x0, x1, x2, x3, x4);     // P_0: next global pixel in the row
+      st[0][j] = x0; st[1][j] = x1; st[2][j] = x2; st[3][j] = x3; st[4][j] = x4;
+    }
+    const uint32_t id = id0 + h * 64u;
+    *reinterpret_cast<uint4 *>(A.rng + id) = d;
+    *reinterpret_cast<uint4 *>(A.rng + id + 4) = d;
+#pragma unroll
+    for (int w = 0; w < 5; ++w) {
+      uint4 *o = reinterpret_cast<uint4 *>(A.rng + static_cast<size_t>(w + 1) * n + id);
+      o[0] = make_uint4(st[w][0], st[w][1], st[w][2], st[w][3]);
+      o[1] = make_uint4(st[w][4], st[w][5], st[w][6], st[w][7]);
+    }
   }
 }
 

@@ -91,6 +91,19 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
   return true;
 }
 
+// The complete hipRTC option vector.  Same numerics flags as the offline build.  SLP vectorisation is
+// off: on this code it packs scalar f32 pairs into v_pk_* with extra moves, turns the planar inside-test
+// into a <4 x i1> reduction, and its longer live ranges spill ~100 SGPRs (measured: -10% instructions,
+// 86 -> 71 VGPRs on scene 0; measured again in round 1: +30 % frame time).  RT_JIT_OPTS appends options
+// (A/B experiments); hipRTC keeps the FIRST of two conflicting flags, so it cannot override these.
+// The on-disk cache key hashes this whole vector (build_module): bit-exact parity rests on these flags.
+std::vector<std::string> jit_options(const std::string &arch) {
+  std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                                "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
+  for (const std::string &x : jit_extra_options()) o.push_back(x);
+  return o;
+}
+
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log) {
   hiprtcProgram prog;
   const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
@@ -99,14 +112,7 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
     if (log) *log = "hiprtcCreateProgram failed";
     return false;
   }
-  // Same numerics flags as the offline build.  SLP vectorisation is off: on this code it packs
-  // scalar f32 pairs into v_pk_* with extra moves, turns the planar inside-test into a <4 x i1>
-  // reduction, and its longer live ranges spill ~100 SGPRs (measured: -10% instructions, 86 -> 71
-  // VGPRs on scene 0; measured again in round 1: +30 % frame time).  RT_JIT_OPTS appends options (A/B
-  // experiments); hipRTC keeps the FIRST of two conflicting flags, so it cannot override these.
-  std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                                "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
-  for (const std::string &x : jit_extra_options()) o.push_back(x);
+  const std::vector<std::string> o = jit_options(arch);
   std::vector<const char *> opts;
   for (const std::string &x : o) opts.push_back(x.c_str());
   const hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(opts.size()), opts.data());
@@ -169,7 +175,7 @@ bool make_dirs(const std::string &d) {
   return true;
 }
 
-constexpr char kCacheMagic[8] = {'R', 'T', 'J', 'I', 'T', 'C', 'O', '1'};
+constexpr char kCacheMagic[8] = {'R', 'T', 'J', 'I', 'T', 'C', 'O', '2'};
 
 bool disk_load(const std::string &path, const std::string &key, std::vector<char> *code) {
   FILE *f = std::fopen(path.c_str(), "rb");
@@ -204,11 +210,17 @@ void disk_store(const std::string &dir, const std::string &path, const std::stri
   if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());   // atomic publish
 }
 
+// Everything outside the source that decides the code object: hipRTC major.minor, the HIP runtime's full
+// version (it carries the patch level, i.e. the bundled compiler build), the version this library was
+// built against, and the embedded device headers.
 std::string toolchain_tag() {
-  int major = 0, minor = 0;
+  int major = 0, minor = 0, runtime = 0;
   hiprtcVersion(&major, &minor);
+  if (hipRuntimeGetVersion(&runtime) != hipSuccess) runtime = -1;
   static const std::string headers = std::to_string(fnv1a(std::string(kEmbedLayout) + '\x01' + kEmbedBody));
-  return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " headers " + headers;
+  return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " runtime " + std::to_string(runtime) +
+         " built " + std::to_string(HIP_VERSION_MAJOR) + "." + std::to_string(HIP_VERSION_MINOR) + "." +
+         std::to_string(HIP_VERSION_PATCH) + " headers " + headers;
 }
 
 // Compile (or fetch) the module of `src` exporting <prefix>_render, <prefix>_render_count, <prefix>_probe.
@@ -218,7 +230,7 @@ bool build_module(const std::string &src, const std::string &prefix, JitKernels 
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const std::string arch = arch_of(dev);
   std::string opts;
-  for (const std::string &x : jit_extra_options()) opts += x + " ";
+  for (const std::string &x : jit_options(arch)) opts += x + " ";
   const std::string disk_key = arch + "|" + toolchain_tag() + "|" + opts + "|" + src;
   const std::string key = std::to_string(dev) + "|" + disk_key;
   std::lock_guard<std::mutex> lock(g_mu);
@@ -329,6 +341,26 @@ std::string jit_accel_source(const SceneImage &img, int variant) {
          std::to_string(v | kVarProbe) + ", " + at + ">(A);\n}\n";
   src += "}  // namespace rt\n";
   return src;
+}
+
+std::string jit_mixed_source(const SceneImage &img, int variant) {
+  const int v = variant & kJitVarMask;
+  const std::string mt = "MixedTraceK<" + std::to_string(scene_kinds(img)) + "u>";
+  std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr() + " void rt_mixed_render(RenderArgs A) {\n  render_body<" +
+         std::to_string(v | kVarNoProbe) + ", " + mt + ">(A);\n}\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_mixed_render_count(RenderArgs A) {\n  render_body<" +
+         std::to_string(v | kVarCount | kVarNoProbe) + ", " + mt + ">(A);\n}\n";
+  src += "extern \"C\" __global__ __launch_bounds__(256) void rt_mixed_probe(RenderArgs A) {\n  render_body<" +
+         std::to_string(v | kVarProbe) + ", " + mt + ">(A);\n}\n";
+  src += "}  // namespace rt\n";
+  return src;
+}
+
+bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
+  out->visits = 0;
+  out->folded = false;
+  return build_module(jit_mixed_source(img, variant), "rt_mixed", out, why);
 }
 
 bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {

@@ -38,12 +38,17 @@ std::string jit_lane_source(const SceneImage &img, int variant);
 // Verified sphere traversal kernels (AccelTraceK over the scene's node kinds for the fallback walk).
 bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
 std::string jit_accel_source(const SceneImage &img, int variant);
+// verified mixed-world traversal kernels (MixedTraceK over the scene's node kinds)
+bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
+std::string jit_mixed_source(const SceneImage &img, int variant);
 uint32_t scene_kinds(const SceneImage &img);
 // material / texture kinds present, as variant bits (kVarMatShift / kVarTexShift)
 int scene_shading_bits(const SceneImage &img);
 
 // extra hipRTC options from the RT_JIT_OPTS environment variable (space separated)
 std::vector<std::string> jit_extra_options();
+// the complete hipRTC option vector for `arch` (numerics flags + RT_JIT_OPTS); hashed into the disk-cache key
+std::vector<std::string> jit_options(const std::string &arch);
 
 hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes);

@@ -17,156 +17,17 @@
 #include <limits>
 #include <vector>
 
+#include "accel_build.h"
 #include "gpu_scene.h"
 
 namespace rt {
 namespace {
 
-inline float fl(uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; }
-inline uint32_t fb(float f) { uint32_t b; std::memcpy(&b, &f, 4); return b; }
-
-struct Prim {
-  double lo[3], hi[3], c[3];   // padded bounds over the motion, centroid
-  double m;                    // |c0| + |mv| + r: bounds |centre(t)| + r
-  uint32_t node;               // reference record
-  float vbox[6];               // deepest reference BVH ancestor box (x0 x1 y0 y1 z0 z1)
-};
-
-struct Box {
-  double lo[3] = {std::numeric_limits<double>::infinity(), std::numeric_limits<double>::infinity(),
-                  std::numeric_limits<double>::infinity()};
-  double hi[3] = {-std::numeric_limits<double>::infinity(), -std::numeric_limits<double>::infinity(),
-                  -std::numeric_limits<double>::infinity()};
-  void grow(const double *l, const double *h) {
-    for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], l[a]); hi[a] = std::max(hi[a], h[a]); }
-  }
-  double area() const {
-    const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-    if (!(dx >= 0)) return 0.0;
-    return 2.0 * (dx * dy + dy * dz + dz * dx);
-  }
-};
-
-// float bounds that contain the double box (rounded outward)
-inline float down(double x) {
-  float f = static_cast<float>(x);
-  if (static_cast<double>(f) > x) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
-  return f;
-}
-inline float up(double x) {
-  float f = static_cast<float>(x);
-  if (static_cast<double>(f) < x) f = std::nextafter(f, std::numeric_limits<float>::infinity());
-  return f;
-}
-
-struct Builder {
-  std::vector<Prim> prims;
-  std::vector<uint32_t> nodes;   // kAccelNodeWords per node
-  std::vector<uint32_t> order;   // prim order of the leaves
-  uint32_t max_depth = 0;
-
-  static constexpr int kBins = 16;
-  // SAH constants (A/B knobs RT_ACCEL_LEAF = max spheres per leaf, RT_ACCEL_ISECT = sphere test cost
-  // relative to a node visit)
-  uint32_t kMaxLeaf = 4;
-  double kTravCost = 1.0, kIsectCost = 1.5;
-
-  // returns the child reference; fills its box and M
-  uint32_t build(uint32_t b, uint32_t e, uint32_t depth, Box *box_out, double *m_out) {
-    max_depth = std::max(max_depth, depth);
-    Box bb, cb;
-    double m = 0.0;
-    for (uint32_t i = b; i < e; ++i) {
-      bb.grow(prims[i].lo, prims[i].hi);
-      cb.grow(prims[i].c, prims[i].c);
-      m = std::max(m, prims[i].m);
-    }
-    *box_out = bb;
-    *m_out = m;
-    const uint32_t n = e - b;
-    auto leaf = [&]() {
-      const uint32_t first = static_cast<uint32_t>(order.size());
-      for (uint32_t i = b; i < e; ++i) order.push_back(i);
-      return kAccelLeaf | ((n - 1) << 24) | first;
-    };
-    if (n <= 1) return leaf();
-    // binned SAH over centroids
-    int best_axis = -1, best_split = -1;
-    double best_cost = std::numeric_limits<double>::infinity();
-    for (int a = 0; a < 3; ++a) {
-      const double ext = cb.hi[a] - cb.lo[a];
-      if (!(ext > 0)) continue;
-      Box bin[kBins];
-      uint32_t cnt[kBins] = {0};
-      for (uint32_t i = b; i < e; ++i) {
-        int k = static_cast<int>((prims[i].c[a] - cb.lo[a]) / ext * kBins);
-        k = std::min(std::max(k, 0), kBins - 1);
-        bin[k].grow(prims[i].lo, prims[i].hi);
-        cnt[k]++;
-      }
-      double right_area[kBins];
-      uint32_t right_cnt[kBins];
-      Box acc;
-      uint32_t c = 0;
-      for (int k = kBins - 1; k > 0; --k) {
-        if (cnt[k]) acc.grow(bin[k].lo, bin[k].hi);
-        c += cnt[k];
-        right_area[k] = acc.area();
-        right_cnt[k] = c;
-      }
-      Box lacc;
-      uint32_t lc = 0;
-      for (int k = 0; k < kBins - 1; ++k) {
-        if (cnt[k]) lacc.grow(bin[k].lo, bin[k].hi);
-        lc += cnt[k];
-        if (lc == 0 || right_cnt[k + 1] == 0) continue;
-        const double cost = lacc.area() * lc + right_area[k + 1] * right_cnt[k + 1];
-        if (cost < best_cost) { best_cost = cost; best_axis = a; best_split = k; }
-      }
-    }
-    const double parent_area = std::max(bb.area(), 1e-30);
-    const double split_cost = kTravCost + kIsectCost * best_cost / parent_area;
-    const double leaf_cost = kIsectCost * n;
-    if (n <= kMaxLeaf && (best_axis < 0 || leaf_cost <= split_cost)) return leaf();
-    uint32_t mid;
-    if (best_axis >= 0) {
-      const int a = best_axis;
-      const double ext = cb.hi[a] - cb.lo[a];
-      auto it = std::partition(prims.begin() + b, prims.begin() + e, [&](const Prim &p) {
-        int k = static_cast<int>((p.c[a] - cb.lo[a]) / ext * kBins);
-        k = std::min(std::max(k, 0), kBins - 1);
-        return k <= best_split;
-      });
-      mid = static_cast<uint32_t>(it - prims.begin());
-    } else {
-      mid = b + n / 2;   // coincident centroids: split the list
-    }
-    if (mid == b || mid == e) mid = b + n / 2;
-    const uint32_t idx = static_cast<uint32_t>(nodes.size() / kAccelNodeWords);
-    nodes.resize(nodes.size() + kAccelNodeWords, 0);
-    Box lb, rb;
-    double lm, rm;
-    const uint32_t l = build(b, mid, depth + 1, &lb, &lm);
-    const uint32_t r = build(mid, e, depth + 1, &rb, &rm);
-    uint32_t *w = &nodes[static_cast<size_t>(idx) * kAccelNodeWords];
-    const Box *cbx[2] = {&lb, &rb};
-    const double mm[2] = {lm, rm};
-    for (int c = 0; c < 2; ++c) {
-      // stored pre-padded by the subtree's share of the cone padding, kAccelKappa * M (the ray's
-      // share, kAccelKappa * |o|_1, is applied in t by the kernel)
-      const double pad = static_cast<double>(kAccelKappa) * mm[c];
-      uint32_t *o = w + 6 * c;
-      o[0] = fb(down(cbx[c]->lo[0] - pad)); o[1] = fb(up(cbx[c]->hi[0] + pad));
-      o[2] = fb(down(cbx[c]->lo[1] - pad)); o[3] = fb(up(cbx[c]->hi[1] + pad));
-      o[4] = fb(down(cbx[c]->lo[2] - pad)); o[5] = fb(up(cbx[c]->hi[2] + pad));
-    }
-    w[12] = l;
-    w[13] = r;
-    w[14] = fb(up(lm));
-    w[15] = fb(up(rm));
-    return idx;
-  }
-};
+using accel::Box;
+using accel::Builder;
+using accel::Prim;
+using accel::fb;
+using accel::fl;
 
 struct Walker {
   const SceneImage &img;

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* status codes */
 #define RT_OK                 0
@@ -84,6 +84,10 @@ typedef struct rt_params {
 #define RT_FLAG_NO_FOLD      0x40u /* RT_TRAV_STATIC without exact constant folding of primitive tests */
 #define RT_FLAG_FORCE_ACCEL  0x80u /* force RT_TRAV_ACCEL (falls back to LANE when the world is not all spheres) */
 #define RT_FLAG_NO_ACCEL     0x100u /* never use RT_TRAV_ACCEL */
+#define RT_FLAG_FORCE_MIXED  0x400u /* force RT_TRAV_MIXED (falls back to LANE when no subtree qualifies) */
+#define RT_FLAG_NO_MIXED     0x800u /* never use RT_TRAV_MIXED */
+#define RT_FLAG_RC_AUDIT     0x200u /* test aid: count the colour-stack levels the render spilled to HBM
+                                       (rt_stats.rc_hbm_slots); costs a fill + a read-back of that buffer */
 
 /* traversal policies (rt_stats.traversal) */
 #define RT_TRAV_LANE   0   /* per-lane DFS over an LDS stack (any scene) */
@@ -91,6 +95,8 @@ typedef struct rt_params {
 #define RT_TRAV_STATIC 2   /* the scene's DFS expanded to straight-line code, compiled with hipRTC */
 #define RT_TRAV_ACCEL  3   /* all-sphere worlds: SAH tree walk, verified against the reference tree per ray
                               (rays it cannot verify take the reference walk; bit-identical records) */
+#define RT_TRAV_MIXED  4   /* worlds with transforms: the reference DFS above the transform-free subtrees, a
+                              verified SAH walk inside them (same fallback rule; bit-identical records) */
 
 /* rt_stats.counters[] slots (filled only with RT_FLAG_COUNT) */
 enum {
@@ -124,6 +130,12 @@ typedef struct rt_stats {
   uint32_t accel_fallbacks; /* rays of the last render the verified traversal re-traced with the reference walk */
   int32_t jit_source;      /* where the last render's run-time kernels came from: RT_JIT_* below */
   double jit_ms;           /* host time the last render spent obtaining them (compile or cache load) */
+  uint64_t rc_hbm_slots;   /* RT_FLAG_RC_AUDIT: distinct HBM colour-stack slots (thread, level) written by the
+                              render — > 0 proves levels past the LDS ones were pushed and unwound (:1253-1276) */
+  int32_t rc_lds_levels;   /* colour-stack levels the last render kept in LDS (deeper ones live in HBM) */
+  int32_t mix_macros;      /* RT_TRAV_MIXED: transform-free subtrees with a SAH walk (0 otherwise) */
+  uint32_t mix_fallbacks;  /* RT_TRAV_MIXED: macro walks of the last render handed back to the reference walk */
+  int32_t pad_;
 } rt_stats;
 
 /* rt_stats.jit_source */
@@ -173,6 +185,9 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
  * would build it (traversal = RT_TRAV_STATIC, RT_TRAV_ACCEL or RT_TRAV_LANE; no device needed):
  * ISA / register / scratch inspection with hipcc (tools/isa_stats.sh). */
 int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap);
+/* Diagnostics for the verified mixed-world traversal (no device needed): info = {macro roots, dynamic
+ * ones, primitives in their SAH trees, deepest SAH tree}; RT_ERR_UNSUPPORTED when no subtree qualifies. */
+int rt_mixed_build(const rt_scene *scene, uint32_t info[4]);
 /* Diagnostics for the verified sphere traversal (no device needed): builds the SAH tree of an
  * all-sphere world.  info = {root node, depth, spheres, node words}; words (if non-null, cap words)
  * receives the node words then the prim words (layout: device/rt_layout.h kAccel*).

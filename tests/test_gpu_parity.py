@@ -678,3 +678,163 @@ def test_cooperative_noise_octaves_vs_oracle(idx, env, monkeypatch):
     fb, st = gpu(w.scene(), cam, p)
     assert st.traversal == rt.RT_TRAV_STATIC
     assert np.array_equal(bits(fb), bits(ref))
+
+
+# ---- colour stack (ray_color's attenuation stack, raytracing.cu:1253-1276,1362-1368) past its LDS levels ----
+# RT_RC_LDS_LEVELS pins the LDS levels low (4, and 5: odd, so the 16-bit kernels' level pairs round up to 6),
+# so every path deeper than that pushes and unwinds HBM levels; RT_FLAG_RC_AUDIT counts the HBM slots the
+# render wrote (> 0 proves the spill path ran) — on every traversal policy, against the oracle
+SPILL_FORCES = [0, rt.RT_FLAG_FORCE_LANE, rt.RT_FLAG_FORCE_PACKET, rt.RT_FLAG_FORCE_STATIC]
+
+
+def _spill_check(w, s, W, H, spp, b, forces, want_levels):
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=b)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    for force in forces:
+        p.flags = force | rt.RT_FLAG_RC_AUDIT
+        fb, st = gpu(w.scene(), cam, p)
+        assert np.array_equal(bits(fb), bits(ref)), (force, st.traversal)
+        assert st.rc_lds_levels in want_levels, (force, st.rc_lds_levels)
+        assert st.rc_hbm_slots > 0, (force, st.traversal)
+
+
+@pytest.mark.parametrize("levels", ["4", "5"])
+@pytest.mark.parametrize("idx,W,H,spp", [(1, 40, 40, 4), (17, 48, 27, 4), (20, 48, 27, 2)])
+def test_colour_stack_hbm_levels_vs_oracle(idx, W, H, spp, levels, monkeypatch):
+    monkeypatch.setenv("RT_RC_LDS_LEVELS", levels)
+    w, s = rt.build_scene(idx)
+    forces = SPILL_FORCES + ([rt.RT_FLAG_FORCE_ACCEL] if idx == 20 else [])
+    _spill_check(w, s, W, H, spp, 50, forces, {int(levels), int(levels) + 1})
+
+
+@pytest.mark.parametrize("levels", ["4", "5"])
+@pytest.mark.parametrize("seed", [1, 6])
+def test_colour_stack_hbm_levels_random_worlds(seed, levels, monkeypatch):
+    monkeypatch.setenv("RT_RC_LDS_LEVELS", levels)
+    w, s = _random_world(seed)
+    # a closed diffuse room around the camera and the random objects: paths end only at lights, at
+    # absorbing metal bounces or at depth 50, so many are deeper than the LDS levels
+    w.box((-20.0, -20.0, -20.0), (20.0, 20.0, 20.0), w.lambert((0.8, 0.75, 0.7)))
+    _spill_check(w, s, 48, 27, 8, 50, SPILL_FORCES, {int(levels), int(levels) + 1})
+
+
+@pytest.mark.parametrize("b", [16, 17])
+@pytest.mark.parametrize("idx", [1, 17])
+def test_deep_unwind_switch_vs_oracle(idx, b, monkeypatch):
+    # max_bounces > kDeepBounces (16) selects the batched HBM unwind (kVarDeep): both sides of the switch
+    monkeypatch.setenv("RT_RC_LDS_LEVELS", "4")
+    w, s = rt.build_scene(idx)
+    _spill_check(w, s, 40, 30, 6, b, [0, rt.RT_FLAG_FORCE_LANE], {4, 5})
+
+
+# ---- verified traversal of mixed worlds (RT_TRAV_MIXED): the reference DFS above the transform-free
+# subtrees, a SAH walk + reach proof inside them (mixed_accel.cpp, MixedTraceK) ----
+def _mixed_world(seed: int):
+    """final_scene-like (raytracing.cu:2151-2202) at random: a grid of boxes of random heights, a cluster of
+    spheres under y-rotation + translation, transformed boxes and pyramids (groups inside transforms), loose
+    quads / triangles / spheres, a light.  Large enough for dynamic macros (>= 64 primitives below nodes
+    with transforms)."""
+    g = np.random.default_rng(5000 + seed)
+    w = rt.World(capacity=4000)
+    ground = w.lambert((0.48, 0.83, 0.53))
+    n = int(g.integers(6, 11))
+    for i in range(n):
+        for j in range(n):
+            x0, z0 = -5.0 + i * 1.0, -5.0 + j * 1.0
+            w.box((x0, 0.0, z0), (x0 + 1.0, float(g.uniform(0.05, 1.2)), z0 + 1.0), ground)
+    mats = [w.lambert((0.73, 0.73, 0.73)), w.metal((0.8, 0.8, 0.9), float(g.uniform(0, 1))), w.dielectric(1.5),
+            w.checker(0.5, (0.2, 0.3, 0.1), (0.9, 0.9, 0.9))]
+    for _ in range(int(g.integers(10, 60))):
+        c = tuple(float(x) for x in g.uniform(0, 1.6, 3))
+        w.sphere(c, 0.1, mats[0], xf=rt.RT_XF_YROTATE_TRANSLATE, angle=15.0, offset=(-1.0, 2.7, 0.95))
+    for _ in range(int(g.integers(1, 5))):
+        a = g.uniform(-3, 3, 3)
+        w.box(tuple(a), tuple(a + g.uniform(0.3, 1.0, 3)), mats[int(g.integers(0, 4))],
+              xf=int(g.integers(1, 4)), angle=float(g.uniform(-90, 90)), offset=tuple(float(x) for x in g.uniform(-1, 1, 3)))
+    a = g.uniform(-2, 2, 3)
+    w.pyramid(tuple(a), (float(a[0] + 1), float(a[1]), float(a[2] + 1)), (float(a[0] + 0.5), float(a[1] + 1), float(a[2] + 0.5)),
+              mats[0], xf=rt.RT_XF_YROTATE, angle=30.0)
+    for _ in range(int(g.integers(1, 6))):
+        c = tuple(float(x) for x in g.uniform(-3, 3, 3))
+        k = int(g.integers(0, 3))
+        if k == 0:
+            w.sphere(c, float(g.uniform(0.2, 0.8)), mats[int(g.integers(0, 4))])
+        elif k == 1:
+            w.quad(c, tuple(float(x) for x in g.uniform(-1, 1, 3)), tuple(float(x) for x in g.uniform(-1, 1, 3)), mats[0])
+        else:
+            w.triangle(c, tuple(float(x) for x in g.uniform(-1, 1, 3)), tuple(float(x) for x in g.uniform(-1, 1, 3)), mats[3])
+    w.quad((-1.0, 4.5, -1.0), (2.0, 0.0, 0.0), (0.0, 0.0, 2.0), w.light((7.0, 7.0, 7.0)))
+    s = rt.Settings()
+    _abi.host_lib().rt_settings_default(C.byref(s))
+    s.lookfrom = rt.vec3(float(g.uniform(-6, 6)), float(g.uniform(2, 5)), float(g.uniform(-9, -6)))
+    s.lookat = rt.vec3(0.0, 1.0, 0.0)
+    s.vfov = float(g.uniform(30, 60))
+    s.background = rt.vec3(*((0.0, 0.0, 0.0) if seed % 2 else (0.5, 0.6, 0.8)))
+    return w, s
+
+
+def test_mixed_traversal_final_scene_vs_oracle():
+    w, s = rt.build_scene(3)   # final_scene: 400 boxes, 1000 rotated + translated spheres
+    info = rt.mixed_build(w.scene())
+    assert info and info["macros"] > 0 and info["dynamic"] > 0
+    cam, W, H = rt.camera_from_settings(s, 80, 80)
+    p = rt.make_params(s, W, H, spp=3, bounces=40)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_MIXED and st.mix_macros == info["macros"]
+    assert np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("seed", list(range(int(__import__("os").environ.get("RT_FUZZ_SEEDS", "12")) // 2)))
+def test_random_mixed_worlds_verified_walk(seed):
+    w, s = _mixed_world(seed)
+    assert rt.mixed_build(w.scene())
+    cam, W, H = rt.camera_from_settings(s, 64, 36)
+    p = rt.make_params(s, W, H, spp=4, bounces=12)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    p.flags = rt.RT_FLAG_FORCE_MIXED
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_MIXED
+    assert np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("seed", [3, 7, 9])
+def test_random_scenes_forced_mixed_walk(seed):
+    # the small random worlds of test_random_scenes_vs_oracle through the mixed walk (static macros only)
+    w, s = _random_world(seed)
+    cam, W, H = rt.camera_from_settings(s, 48, 27)
+    p = rt.make_params(s, W, H, spp=4, bounces=10)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    p.flags = rt.RT_FLAG_FORCE_MIXED
+    fb, st = gpu(w.scene(), cam, p)
+    assert np.array_equal(bits(fb), bits(ref)), st.traversal
+
+
+def test_mixed_walk_fallback_path_vs_oracle(monkeypatch):
+    # RT_MIX_PROVE=0: every macro walk is handed back to the reference's expansion of its root
+    monkeypatch.setenv("RT_MIX_PROVE", "0")
+    w, s = _mixed_world(1)
+    cam, W, H = rt.camera_from_settings(s, 48, 27)
+    p = rt.make_params(s, W, H, spp=3, bounces=10, flags=rt.RT_FLAG_FORCE_MIXED)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    fb, st = gpu(w.scene(), cam, p)
+    assert rc == 0 and st.traversal == rt.RT_TRAV_MIXED and st.mix_fallbacks > 0
+    assert np.array_equal(bits(fb), bits(ref))
+
+
+def test_mixed_walk_final_scene_full_size_rows():
+    # the final_scene frame (800x800, d40) at reduced spp: every 61st row (first and last) vs the oracle
+    w, s = rt.build_scene(3)
+    cam, W, H = rt.camera_from_settings(s, 800, 800)
+    full, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=2, bounces=40))
+    assert st.traversal == rt.RT_TRAV_MIXED
+    stride = 47
+    p = rt.make_params(s, W, H, spp=2, bounces=40, row_offset=0, row_stride=stride, row_count=(H - 1) // stride + 1)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    assert np.array_equal(bits(full[0::stride]), bits(ref))
