@@ -331,6 +331,8 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
 // compact colour stack (rt_layout.h kRcRecTag): a level holds a code of its attenuation
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t rc_rec(uint32_t r, bool wide) { return wide ? (kRcRecTag | r) : r; }
+// a wide code is a grey unless it is a record (exponent field all ones) or a texel (sign bit)
+__device__ __forceinline__ bool rc_is_grey(uint32_t w) { return (w & kRcTexelTag) == 0 && (w & kRcRecTag) != kRcRecTag; }
 
 // texture_color's resolution (checker recursion, image clamp, noise) returning the colour-stack code of
 // the Lambertian attenuation instead of the colour: rc_decode(code) == texture_color(...) bit for bit
@@ -368,7 +370,7 @@ __device__ uint32_t texture_code(const Mem<LDS> &S, const RenderArgs &A, uint32_
         y = (y < 0) ? 0 : ((y > ht) ? ht : y);
         uint64_t wo = static_cast<uint64_t>(t0.w) + 3ull * (static_cast<uint64_t>(y) * wd + x);
         if (wo + 3 > A.pixel_words) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
-        return kRcTexelTag | static_cast<uint32_t>(wo);   // UV kernels are wide; pixel pool < 2^23 words
+        return kRcTexelTag | static_cast<uint32_t>(wo);   // UV kernels are wide; pixel pool < 2^31 words
       }
       case T_NOISE: {
         if (!NOISE || !(TM & (1u << T_NOISE))) return rc_rec(A.rc_consts + RC_BLACK, WIDE);
@@ -400,14 +402,14 @@ __device__ uint32_t texture_code(const Mem<LDS> &S, const RenderArgs &A, uint32_
 // code -> attenuation (the record's words 1..3, the texel, or the grey)
 template <bool LDS, bool WIDE, bool NOISE, bool UV>
 __device__ __forceinline__ f3 rc_decode(const Mem<LDS> &S, const RenderArgs &A, uint32_t w) {
-  const bool grey = NOISE && (w & kRcRecTag) != kRcRecTag;   // a grey reads record 0 (in bounds), unused
+  const bool grey = NOISE && rc_is_grey(w);   // a grey reads record 0 (in bounds), unused
   if (!WIDE || !UV) {
     const uint32_t r = grey ? 0u : (WIDE ? (w & kRcPayload) : w);
     const uint4 q = S.w4(A.off_mats + r * kRecWords);
     return grey ? mk(asf(w), asf(w), asf(w)) : mk(asf(q.y), asf(q.z), asf(q.w));
   }
-  const bool texel = (w & kRcTexelTag) == kRcTexelTag;
-  const uint32_t o = grey ? A.off_mats : (texel ? A.off_pixels + (w & kRcPayload) : A.off_mats + (w & kRcPayload) * kRecWords + 1);
+  const bool texel = (w & kRcTexelTag) != 0;
+  const uint32_t o = grey ? A.off_mats : (texel ? A.off_pixels + (w & kRcTexelPayload) : A.off_mats + (w & kRcPayload) * kRecWords + 1);
   const f3 c = mk(S.f(o), S.f(o + 1), S.f(o + 2));
   return grey ? mk(asf(w), asf(w), asf(w)) : c;
 }
@@ -420,7 +422,7 @@ __device__ __forceinline__ void rc_decode_batch(const Mem<LDS> &S, const RenderA
   if (NOISE) {
     bool rec = false;
 #pragma unroll
-    for (int i = 0; i < N; ++i) rec |= (cw[i] & kRcRecTag) == kRcRecTag;
+    for (int i = 0; i < N; ++i) rec |= !rc_is_grey(cw[i]);
     if (__ballot(rec) == 0) {
 #pragma unroll
       for (int i = 0; i < N; ++i) at[i] = mk(asf(cw[i]), asf(cw[i]), asf(cw[i]));
@@ -993,7 +995,8 @@ struct AccelTraceK {
 // (sphere) or v <= tmax (quad, triangle: :1066).  The walk keeps
 //   best    the smallest v below min(best, tmax_in), with its deepest reference BVH ancestor A below the
 //           macro root (its "group": every primitive under that node shares it),
-//   tie     some candidate equal to min(best, tmax_in) (the reference's order would decide),
+//   tie     a second candidate equal to the final min(best, tmax_in) (the reference's order would decide
+//           which one it keeps; equal candidates above the final value are all replaced by it),
 //   second  a lower bound on v over the primitives outside best's group (pruning bound included),
 // and proves reach: the reference visits A with the tmax of that moment, T_A = min(tmax_in, v of the
 // primitives it accepted before A), all outside A's subtree, so T_A >= lb = min(tmax_in, second, bound);
@@ -1099,28 +1102,54 @@ struct MixedTraceK {
         } else if ((KM & (1u << K_SPHERE)) && kind == K_SPHERE) {
           sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
                          asf(w2.y), asf(w2.z), in_xf);
-        } else if ((KM & (1u << K_TRANSLATE)) && kind == K_TRANSLATE) {
-          const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
-          if (T.tc == 0) {
-            translate_enter(T, r, off);
-            stk[sp * 64] = static_cast<uint16_t>(idx);
-            stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
-            sp += 2;
-            T.tc++;
+        } else if ((KM & ((1u << K_TRANSLATE) | (1u << K_YROTATE))) && (kind == K_TRANSLATE || kind == K_YROTATE)) {
+          const bool tr = kind == K_TRANSLATE;
+          const uint32_t chain = w3.x;   // W_MACRO: fused chain marker
+          if ((tr ? T.tc : T.yc) == 0 && (chain & kChainFused)) {
+            // translate -> [y-rotate ->] primitive, or y-rotate -> primitive: the reference's enter, enter,
+            // test, cleanup, cleanup steps (:1176-1237, in this order, nothing else runs in between) at once
+            const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
+            const bool rot = !tr || (chain & kChainRotate);
+            float sn = asf(w0.z), cs = asf(w0.w);
+            if (tr) {
+              translate_enter(T, r, off);
+              if (rot) { const uint4 c0 = S.w4(w0.y * kNodeWords); sn = asf(c0.z); cs = asf(c0.w); }
+            }
+            if (rot) rotate_enter(T, r, sn, cs);
+            const uint32_t gb = (chain & kChainPrimMask) * kNodeWords;
+            const uint4 g0 = S.w4(gb), g1 = S.w4(gb + 4), g2 = S.w4(gb + 8), g3 = S.w4(gb + 12), g4 = S.w4(gb + 16);
+            if ((KM & (1u << K_SPHERE)) && g0.x == K_SPHERE)
+              sphere_hit<UV>(T, r, h, g0.y, mk(asf(g0.z), asf(g0.w), asf(g1.x)), mk(asf(g1.y), asf(g1.z), asf(g1.w)),
+                             asf(g2.y), asf(g2.z), true);
+            else
+              planar_hit(T, r, h, g0.x == K_TRIANGLE, g0.y, mk(asf(g0.z), asf(g0.w), asf(g1.x)), asf(g1.y),
+                         mk(asf(g1.z), asf(g1.w), asf(g2.x)), mk(asf(g2.y), asf(g2.z), asf(g2.w)),
+                         mk(asf(g3.x), asf(g3.y), asf(g3.z)), mk(asf(g3.w), asf(g4.x), asf(g4.y)), true);
+            if (rot) rotate_exit(T, r, h, sn, cs);
+            if (tr) translate_exit(T, r, h, off);
+          } else if (tr) {
+            const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
+            if (T.tc == 0) {
+              translate_enter(T, r, off);
+              stk[sp * 64] = static_cast<uint16_t>(idx);
+              stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+              sp += 2;
+              T.tc++;
+            } else {
+              T.tc--;
+              translate_exit(T, r, h, off);
+            }
           } else {
-            T.tc--;
-            translate_exit(T, r, h, off);
-          }
-        } else if ((KM & (1u << K_YROTATE)) && kind == K_YROTATE) {
-          if (T.yc == 0) {
-            rotate_enter(T, r, asf(w0.z), asf(w0.w));
-            stk[sp * 64] = static_cast<uint16_t>(idx);
-            stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
-            sp += 2;
-            T.yc++;
-          } else {
-            T.yc--;
-            rotate_exit(T, r, h, asf(w0.z), asf(w0.w));
+            if (T.yc == 0) {
+              rotate_enter(T, r, asf(w0.z), asf(w0.w));
+              stk[sp * 64] = static_cast<uint16_t>(idx);
+              stk[(sp + 1) * 64] = static_cast<uint16_t>(w0.y);
+              sp += 2;
+              T.yc++;
+            } else {
+              T.yc--;
+              rotate_exit(T, r, h, asf(w0.z), asf(w0.w));
+            }
           }
         }
         if (expand) {
@@ -1200,6 +1229,7 @@ struct MixedTraceK {
             if (best < __builtin_huge_valf() && g != bgroup) second = fminf(second, best);
             best = v; bprim = pr; bgroup = g;
             cur_k = v;
+            tie = false;   // a tie at a larger value no longer matters: the reference ends on this one
           } else if (v == cur_k) {
             tie = true;
           } else if (g != bgroup) {
@@ -1245,7 +1275,10 @@ struct MixedTraceK {
           if (T.tc || T.yc) T.was_last = 1;
         }
       } else {   // the reference's own expansion of the macro root (its box test already passed)
-        if (A.mix_fallbacks) atomicAdd(A.mix_fallbacks, 1u);   // rare (diagnostic)
+        if (A.mix_fallbacks) {   // rare (diagnostic): total, then by reason (tie | reach) in the next words
+          atomicAdd(A.mix_fallbacks, 1u);
+          atomicAdd(A.mix_fallbacks - 9 + (tie ? 0 : 1), 1u);
+        }
         const uint32_t nb = mroot * kNodeWords;
         const uint4 w0 = S.w4(nb);
         int sp = T.sp;

@@ -50,6 +50,10 @@ constexpr int W_MACRO = 12, W_XFBOX = 13;
 constexpr uint32_t kMacroStatic = 0x80000000u, kMacroDynamic = 0x40000000u, kMacroRootMask = 0x00ffffffu;
 // Mixed prims (leaf order): words 0..19 = the primitive's node record (kind, material, geometry), MP_GROUP =
 // its deepest reference BVH ancestor below the macro root (~0u: none), MP_GBOX..+5 = that ancestor's box
+// Transform chains (translate -> [y-rotate ->] primitive, or y-rotate -> primitive): W_MACRO of the head
+// record = kChainFused [| kChainRotate: the translate's child is a y-rotation] | the primitive's record.
+// MixedTraceK runs the reference's five stack steps of such a chain (:1176-1237) as one.
+constexpr uint32_t kChainFused = 0x20000000u, kChainRotate = 0x10000000u, kChainPrimMask = 0x0000ffffu;
 constexpr int kMixPrimWords = 32;
 enum : int { MP_GROUP = 20, MP_GBOX = 21, MP_RECORD = 27 };
 constexpr uint32_t kMixNoGroup = 0xffffffffu;
@@ -71,10 +75,13 @@ constexpr int kTexWords = 8;
 constexpr int kRecWords = 8;
 enum : uint32_t { RC_MAGENTA = 0, RC_BLACK = 1, RC_NAN = 2, kRcConsts = 3 };
 // Colour-stack codes (ray_color's attenuation stack, :1253-1276).  Every attenuation the reference
-// pushes is a record's colour, a texel, or a noise grey (r = g = b); a level stores a code for it:
-//   wide (32 bit):  grey float bits (finite) | kRcRecTag + record | kRcTexelTag + texel word offset
+// pushes is a record's colour, a texel, or a noise grey (r = g = b, 0.5 (1 + sin) >= +0, never negative);
+// a level stores a code for it:
+//   wide (32 bit):  grey float bits (finite, sign bit clear) | kRcRecTag + record (23 bits) |
+//                   kRcTexelTag + texel word offset (31 bits: the whole 2^31-word pixel pool)
 //   narrow (16 bit, scenes without noise and texels and < 65536 records): the record index
-constexpr uint32_t kRcRecTag = 0x7F800000u, kRcTexelTag = 0xFF800000u, kRcPayload = 0x007FFFFFu;
+constexpr uint32_t kRcRecTag = 0x7F800000u, kRcPayload = 0x007FFFFFu;
+constexpr uint32_t kRcTexelTag = 0x80000000u, kRcTexelPayload = 0x7FFFFFFFu;
 static_assert(kMatWords == kRecWords && kTexWords == kRecWords, "colour records are 8 words");
 enum : uint32_t { T_SOLID = 0, T_CHECKER = 1, T_IMAGE = 2, T_NOISE = 3 };
 enum : int {

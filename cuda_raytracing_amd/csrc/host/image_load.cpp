@@ -7,6 +7,7 @@
 // BMP (BI_RGB, 24 and 32 bit) and TGA (uncompressed true-colour and grey, 8/24/32 bit) — with the same
 // output convention.  A file that exists in another format (JPEG, PNG, ...) is RT_ERR_UNSUPPORTED; a file
 // that does not exist is the reference's failed load (no pixels: the texture renders magenta, :346-347).
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -19,14 +20,14 @@ namespace {
 
 // stbi__ldr_to_hdr: (float) pow(c / 255.0f, stbi__l2h_gamma = 2.2f) * stbi__l2h_scale = 1.0f, in float
 // (the float overload of pow in a C++ translation unit)
+// (a function-local static initialised once, thread-safely: worlds may be built concurrently)
 const float *ldr_table() {
-  static float t[256];
-  static bool init = false;
-  if (!init) {
-    for (int c = 0; c < 256; ++c) t[c] = std::pow(static_cast<float>(c) / 255.0f, 2.2f) * 1.0f;
-    init = true;
-  }
-  return t;
+  static const std::array<float, 256> t = [] {
+    std::array<float, 256> v{};
+    for (int c = 0; c < 256; ++c) v[c] = std::pow(static_cast<float>(c) / 255.0f, 2.2f) * 1.0f;
+    return v;
+  }();
+  return t.data();
 }
 
 struct Reader {

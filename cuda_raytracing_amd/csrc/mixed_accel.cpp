@@ -194,6 +194,8 @@ bool build_mixed_accel(SceneImage *img, MixedAccel *out, std::string *why) {
   an.analyse(img->root);
   if (!an.ok) { if (why) *why = "unexpected record kind"; return false; }
   // macro roots: static (transform-free node below a node with transforms, or the root) and dynamic
+  uint32_t dyn_min = kDynMinPrims;   // RT_MIX_DYN_MIN (A/B): primitives below a node for a dynamic macro
+  if (const char *e = std::getenv("RT_MIX_DYN_MIN")) dyn_min = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   std::vector<uint32_t> roots;
   std::vector<uint8_t> dyn;
   {
@@ -208,7 +210,7 @@ bool build_mixed_accel(SceneImage *img, MixedAccel *out, std::string *why) {
       if (k == K_TRANSLATE || k == K_YROTATE) { st.push_back(an.node(r)[W_AUX]); continue; }
       if (k != K_BVH && k != K_GROUP) continue;
       if (an.tf[r] == 1) { roots.push_back(r); dyn.push_back(0); continue; }   // static: whole subtree
-      if (an.nprims[r] >= kDynMinPrims && an.has_xf[r]) { roots.push_back(r); dyn.push_back(1); }
+      if (an.nprims[r] >= dyn_min && an.has_xf[r]) { roots.push_back(r); dyn.push_back(1); }
       an.children(r, &ch);
       for (uint32_t c : ch) st.push_back(c);
     }
@@ -249,6 +251,20 @@ bool build_mixed_accel(SceneImage *img, MixedAccel *out, std::string *why) {
   }
   if (out->macros == 0) { if (why) *why = "no transform-free subtree"; return false; }
   if (bd.nodes.size() / kAccelNodeWords >= 65536) { if (why) *why = "SAH trees too large for u16 stack entries"; return false; }
+  // transform chains ending in a primitive: one fused step in the kernel (W_MACRO of the chain's head)
+  for (uint32_t r = 0; r < img->node_count; ++r) {
+    uint32_t *w = &img->words[static_cast<size_t>(r) * kNodeWords];
+    if (w[W_KIND] != K_TRANSLATE && w[W_KIND] != K_YROTATE) continue;   // words 12..19 unused by both
+    const uint32_t c = w[W_AUX];
+    if (c >= img->node_count) continue;
+    const uint32_t ck = an.node(c)[W_KIND];
+    if (Analysis::is_prim(ck)) {
+      w[W_MACRO] = kChainFused | c;
+    } else if (w[W_KIND] == K_TRANSLATE && ck == K_YROTATE) {
+      const uint32_t g = an.node(c)[W_AUX];
+      if (g < img->node_count && Analysis::is_prim(an.node(g)[W_KIND])) w[W_MACRO] = kChainFused | kChainRotate | g;
+    }
+  }
   for (uint32_t r = 0; r < img->node_count; ++r) {
     uint32_t *w = &img->words[static_cast<size_t>(r) * kNodeWords];
     if (w[W_KIND] != K_BVH && w[W_KIND] != K_GROUP) continue;   // primitives use words 12..19

@@ -148,6 +148,7 @@ struct rt_context {
   bool mixed_ok = false;
   uint32_t mix_nodes = 0, mix_prims = 0;
   bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
+  int static_ok = -1;          // the scene expands within jit_budget (straight-line, stackless traversal); -1 unknown
   DevBuf scene, jump, rng, rc, work, counters, wave_trace, tile_cost, tile_order;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
@@ -330,12 +331,9 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->mix_prims = static_cast<uint32_t>(dev_words.size());
     dev_words.insert(dev_words.end(), c->mixed.prim_words.begin(), c->mixed.prim_words.end());
   }
-  // per-lane u16 stacks of 4 waves x 64 lanes: 512 B per entry; 256 entries (128 KiB) plus the minimum
-  // colour-stack levels is what one 160 KiB block can hold (checked again per render)
-  if (c->img.stack_need > 256) { delete c; return RT_ERR_STACK; }
-  // colour-stack codes carry a record index or a texel word offset in 23 bits (rt_layout.h)
+  // colour-stack codes carry a record index in 23 bits, a texel word offset in 31 (rt_layout.h)
   if (c->img.rec_consts + rt::kRcConsts > rt::kRcPayload ||
-      (c->img.needs_uv && c->img.words.size() - c->img.off_pixels > rt::kRcPayload)) {
+      (c->img.needs_uv && c->img.words.size() - c->img.off_pixels > rt::kRcTexelPayload)) {
     delete c;
     return RT_ERR_UNSUPPORTED;
   }
@@ -398,6 +396,27 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     return RT_OK;
   }
 
+  // Traversal policy (flags; the choice between policies follows below).  Auto: the scene-specialised
+  // straight-line traversal when the scene expands to at most jit_budget node visits (every catalog scene
+  // but the large ones), else the verified SAH walks, else the per-lane DFS.  The wave-packet DFS is kept
+  // as an explicit option (fastest on tiny all-sphere scenes).
+  int trav = c->traversal;
+  if (p->flags & RT_FLAG_FORCE_LANE) trav = RT_TRAV_LANE;
+  else if (p->flags & RT_FLAG_FORCE_PACKET) trav = RT_TRAV_PACKET;
+  else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
+  else if (p->flags & RT_FLAG_FORCE_ACCEL) trav = RT_TRAV_ACCEL;
+  else if (p->flags & RT_FLAG_FORCE_MIXED) trav = RT_TRAV_MIXED;
+  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC || trav == RT_TRAV_ACCEL || trav == RT_TRAV_MIXED))
+    trav = RT_TRAV_LANE;
+  // the straight-line traversal needs no per-lane stack: known before the LDS budget is split
+  if ((trav < 0 || trav == RT_TRAV_STATIC) && c->static_ok < 0) {
+    std::string src;
+    uint32_t v = 0;
+    bool folded = false;
+    c->static_ok = rt::jit_source(c->img, 0, c->jit_budget, false, &src, &v, &folded) ? 1 : 0;
+  }
+  bool stackless = (trav < 0 || trav == RT_TRAV_STATIC) && c->static_ok == 1;
+
   // launch geometry: persistent grid = resident blocks per CU x CUs
   c->lds = c->img.words.size() <= rt::kLdsSceneMaxWords && !(p->flags & RT_FLAG_GLOBAL_SCENE);
   uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
@@ -410,7 +429,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // (the mixed walk keeps a macro's SAH stack above the reference walk's entries)
   const uint32_t stack_cap = std::max({c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u,
                                        c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u});
-  size_t stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
+  const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
+  size_t stack_bytes = stackless ? 0 : full_stack_bytes;
   // one block may declare at most the CU's 160 KiB: a deep per-lane stack first evicts the LDS copy of
   // the scene (read from HBM instead); if the stack and the minimum colour-stack levels alone do not
   // fit, the scene is too deep for this kernel (a status, not a failed launch)
@@ -426,17 +446,6 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
                         (narrow_ok ? rt::kVarNarrow : 0);
-  // Traversal policy.  Auto: the scene-specialised straight-line traversal when the scene expands to
-  // at most jit_budget node visits (every catalog scene but the large random ones), else the per-lane
-  // DFS.  The wave-packet DFS is kept as an explicit option (fastest on tiny all-sphere scenes).
-  int trav = c->traversal;
-  if (p->flags & RT_FLAG_FORCE_LANE) trav = RT_TRAV_LANE;
-  else if (p->flags & RT_FLAG_FORCE_PACKET) trav = RT_TRAV_PACKET;
-  else if (p->flags & RT_FLAG_FORCE_STATIC) trav = RT_TRAV_STATIC;
-  else if (p->flags & RT_FLAG_FORCE_ACCEL) trav = RT_TRAV_ACCEL;
-  else if (p->flags & RT_FLAG_FORCE_MIXED) trav = RT_TRAV_MIXED;
-  if (p->flags & RT_FLAG_NO_JIT && (trav < 0 || trav == RT_TRAV_STATIC || trav == RT_TRAV_ACCEL || trav == RT_TRAV_MIXED))
-    trav = RT_TRAV_LANE;
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
   const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
   if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;
@@ -467,6 +476,16 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     } else {
       c->jit_why = why;
       trav = accel_allowed ? RT_TRAV_ACCEL : (mixed_allowed ? RT_TRAV_MIXED : RT_TRAV_LANE);
+    }
+  }
+  if (!jit_fn && stackless) {   // the straight-line kernel was expected but not obtained: stacks after all
+    stackless = false;
+    stack_bytes = full_stack_bytes;
+    if (rc_bytes + stack_bytes > kLdsPerCu - kLdsReserve) return RT_ERR_STACK;
+    if (c->lds && static_cast<size_t>(scene_lds_words) * 4 + rc_bytes + stack_bytes > kLdsPerCu - kLdsReserve) {
+      c->lds = false;
+      scene_lds_words = 0;
+      c->variant &= ~rt::kVarLds;
     }
   }
   if (trav == RT_TRAV_MIXED) {
@@ -585,7 +604,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
   a.mix_nodes = c->mix_nodes;
   a.mix_prims = c->mix_prims;
-  a.mix_fallbacks = static_cast<uint32_t *>(c->work.p) + 11;
+  a.mix_fallbacks = static_cast<uint32_t *>(c->work.p) + 11;   // reasons at work[2], work[3]
   a.mix_no_proof = c->mix_no_proof ? 1u : 0u;
   a.rc_lds_word = scene_lds_words;
   a.rc_lds_levels = rc_levels;
@@ -659,7 +678,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     pa.wave_trace = nullptr;
     pa.fold_violation = static_cast<uint32_t *>(c->work.p) + 14;   // probe rays: flag ignored
     pa.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 13;  // probe rays: not reported
-    pa.mix_fallbacks = static_cast<uint32_t *>(c->work.p) + 10;
+    pa.mix_fallbacks = nullptr;   // probe rays: not reported
     const hipError_t pe = jit_probe ? rt::jit_launch(jit_probe, pa, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                     : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
                                                         c->lds_bytes, s);
@@ -730,9 +749,13 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   if (c->used_traversal == RT_TRAV_ACCEL &&
       hipMemcpy(&st->accel_fallbacks, static_cast<uint32_t *>(c->work.p) + 12, 4, hipMemcpyDeviceToHost) != hipSuccess)
     return RT_ERR_HIP;
-  if (c->used_traversal == RT_TRAV_MIXED &&
-      hipMemcpy(&st->mix_fallbacks, static_cast<uint32_t *>(c->work.p) + 11, 4, hipMemcpyDeviceToHost) != hipSuccess)
-    return RT_ERR_HIP;
+  if (c->used_traversal == RT_TRAV_MIXED) {
+    uint32_t w[16];
+    if (hipMemcpy(w, c->work.p, sizeof w, hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
+    st->mix_fallbacks = w[11];
+    if (std::getenv("RT_DEBUG"))
+      std::fprintf(stderr, "[rt] mixed walk fallbacks: %u (tie %u, reach %u; probe %u)\n", w[11], w[2], w[3], w[10]);
+  }
   st->init_ms = a;
   st->sched_ms = b;
   st->render_ms = d;

@@ -838,3 +838,26 @@ def test_mixed_walk_final_scene_full_size_rows():
     rc, ref, _ = oracle_render(w.scene(), cam, p)
     assert rc == 0
     assert np.array_equal(bits(full[0::stride]), bits(ref))
+
+
+def test_image_texture_over_2_23_words_vs_oracle():
+    # a texel pool of more than 2^23 words (a 1700x1700 float RGB map, 8.67 M words): colour-stack texel codes
+    # carry 31-bit word offsets, so such scenes render (they were RT_ERR_UNSUPPORTED with 23-bit codes)
+    w = rt.World(capacity=64, arena_bytes=48 << 20)
+    h = wd = 1700
+    yy, xx = np.mgrid[0:h, 0:wd].astype(np.float32)
+    tex = np.stack([xx / (wd - 1), yy / (h - 1), 0.2 + 0.6 * (((xx // 97) + (yy // 89)) % 2)], axis=-1).astype(np.float32)
+    assert tex.size > (1 << 23)
+    img = w.image_pixels(tex)
+    w.sphere((0, 0, -2), 0.8, img)
+    w.quad((-3, -1, -4), (6, 0, 0), (0, 0, 3.5), img)
+    w.sphere((1.2, 0.3, -2.5), 0.5, w.metal((0.8, 0.8, 0.8), 0.1))
+    s = rt.Settings()
+    _abi.host_lib().rt_settings_default(C.byref(s))
+    s.lookfrom, s.lookat, s.vfov = rt.vec3(0, 0.3, 0), rt.vec3(0, 0, -1), 90.0
+    cam, W, H = rt.camera_from_settings(s, 48, 27)
+    p = rt.make_params(s, W, H, spp=4, bounces=8, flags=rt.RT_FLAG_RC_AUDIT)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and len(np.unique(ref.reshape(-1, 3), axis=0)) > 50
+    fb, st = gpu(w.scene(), cam, p)
+    assert np.array_equal(bits(fb), bits(ref))

@@ -74,7 +74,7 @@ static void xfbox_of(const rt_scene *sc, uint16_t r) {
 
 static void dyn_walk(const rt_scene *sc, const ray_t *ray0, double *st);
 enum { S_RAYS, S_VIS_ALL, S_VIS_TOP, S_VIS_TF, S_MACRO, S_K, S_K0, S_LINE_XF, S_PRIM_TOP, S_MACRO_PRIMS,
-       S_LINE_XF_K0, S_DEDUP, S_DTOP, S_DMACRO, S_DMPRIMS, S_DSAH, S_NSTAT };
+       S_LINE_XF_K0, S_DEDUP, S_DTOP, S_DMACRO, S_DMPRIMS, S_DSAH, S_DBVH, S_DBVHPASS, S_DCHAIN, S_DPRIM, S_DGROUP, S_DTOP_K0, S_DRAYS_K0, S_NSTAT };
 
 /* the reference walk, instrumented: a node popped in the top part counts as top, a TF subtree root
  * popped from the top part counts as one macro entry and all its nodes as TF visits */
@@ -182,7 +182,8 @@ static void dyn_walk(const rt_scene *sc, const ray_t *ray0, double *st) {
   int tc = 0, yc = 0;
   static __thread uint8_t inm[STACK_CAP];
   s->data[s->count] = sc->refs[sc->root]; inm[s->count] = 0; s->count++;
-  double top = 0, macro = 0, mprims = 0, sah = 0;
+  double top = 0, macro = 0, mprims = 0, sah = 0, nbvh = 0, nbvhpass = 0, nchain = 0, nprim = 0, ngroup = 0;
+  int K = 0;
   while (s->count > 0) {
     --s->count;
     uint16_t cur = s->data[s->count];
@@ -191,6 +192,10 @@ static void dyn_walk(const rt_scene *sc, const ray_t *ray0, double *st) {
     int child_m = in_m;
     if (!in_m) {
       top++;
+      if (h->kind == RTR_OBJ_BVH) { nbvh++; if (aabb_hit(&h->u.bvh.box, &ray, tmin, tmax)) nbvhpass++; }
+      else if (h->kind == RTR_OBJ_GROUP) ngroup++;
+      else if (h->kind == RTR_OBJ_TRANSLATE || h->kind == RTR_OBJ_YROTATE) nchain++;
+      else nprim++;
       if (h->kind == RTR_OBJ_BVH || h->kind == RTR_OBJ_GROUP) {
         int pass = h->kind == RTR_OBJ_GROUP || aabb_hit(&h->u.bvh.box, &ray, tmin, tmax);
         if (pass && (g_tf[cur] || (g_nprims[cur] >= g_dyn_min && !aabb_hit(&g_xfbox[cur], &ray, tmin, tmax)))) {
@@ -229,7 +234,7 @@ static void dyn_walk(const rt_scene *sc, const ray_t *ray0, double *st) {
       case RTR_OBJ_TRANSLATE: {
         const rtr_translate *tr = &h->u.translate;
         if (in_m) { fprintf(stderr, "chain entered inside a macro!\n"); abort(); }
-        if (tc == 0) { ray.origin = sub(ray.origin, tr->offset); PUSH(cur); PUSH(tr->child); tc++; }
+        if (tc == 0) { ray.origin = sub(ray.origin, tr->offset); PUSH(cur); PUSH(tr->child); tc++; K++; }
         else { ray.origin = add(ray.origin, tr->offset); tc--; }
       } break;
       case RTR_OBJ_YROTATE: {
@@ -253,6 +258,8 @@ static void dyn_walk(const rt_scene *sc, const ray_t *ray0, double *st) {
 #undef PUSH
   }
   free(s);
+  st[S_DBVH] += nbvh; st[S_DBVHPASS] += nbvhpass; st[S_DCHAIN] += nchain; st[S_DPRIM] += nprim; st[S_DGROUP] += ngroup;
+  if (K == 0) { st[S_DTOP_K0] += top; st[S_DRAYS_K0] += 1; }
   st[S_DTOP] += top; st[S_DMACRO] += macro; st[S_DMPRIMS] += mprims; st[S_DSAH] += sah;
 }
 
