@@ -22,7 +22,8 @@ HIP_FLAGS  := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno
               -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-rdc -fno-slp-vectorize -Wall
 ORACLE_FLAGS := -O2 -std=c11 -fPIC -ffp-contract=off -fno-fast-math -fopenmp -Wall -Wextra
 
-HOST_SRC := $(CSRC)/host/rt_host.cpp $(CSRC)/host/image_load.cpp
+HOST_SRC := $(CSRC)/host/rt_host.cpp $(CSRC)/host/image_load.cpp $(CSRC)/host/image_jpeg.cpp \
+            $(CSRC)/host/image_png.cpp
 HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp \
             $(CSRC)/sphere_accel.cpp $(CSRC)/mixed_accel.cpp \
             $(CSRC)/scene_codegen.cpp $(CSRC)/rt_jit.cpp
@@ -36,7 +37,7 @@ hip: $(LIBDIR)/librt_hip.so
 oracle: oracle/_build/liboracle_rt.so
 cli: bin/raytracing
 
-$(LIBDIR)/librt_host.so: $(HOST_SRC) $(CSRC)/host/glibc_rand.h include/rt_host.h include/rt_ref_layout.h include/rt_render.h
+$(LIBDIR)/librt_host.so: $(HOST_SRC) $(CSRC)/host/glibc_rand.h $(CSRC)/host/image_decoders.h include/rt_host.h include/rt_ref_layout.h include/rt_render.h
 	@mkdir -p $(LIBDIR)
 	$(CXX) $(HOST_FLAGS) $(INC) -shared $(HOST_SRC) -o $@
 
@@ -60,9 +61,14 @@ bin/raytracing: $(CSRC)/host/cli.cpp $(LIBDIR)/librt_host.so $(LIBDIR)/librt_hip
 # reference-side checker (test infrastructure): the reference's stb_image compiled where it lies, only
 # when the reference tree is present (not on the GPU box); output only into oracle/_ref/
 REF_INC ?= /root/reference/include
+CLANGXX ?= $(ROCM)/lib/llvm/bin/clang++
 ref:
 	@if [ -f $(REF_INC)/stb_image.h ]; then mkdir -p oracle/_ref && \
-	  $(CXX) -O2 -fPIC -shared -w -I$(REF_INC) oracle/stbi_ref.cpp -o oracle/_ref/libstbi_ref.so; \
+	  $(CXX) -O2 -fPIC -shared -w -I$(REF_INC) oracle/stbi_ref.cpp -o oracle/_ref/libstbi_ref.so && \
+	  $(CLANGXX) -O2 -fPIC -shared -w -ftrivial-auto-var-init=zero -DRT_STBI_FILL=0 -I$(REF_INC) \
+	    oracle/stbi_ref.cpp -o oracle/_ref/libstbi_ref_zero.so && \
+	  $(CLANGXX) -O2 -fPIC -shared -w -ftrivial-auto-var-init=pattern -DRT_STBI_FILL=0xA5 -I$(REF_INC) \
+	    oracle/stbi_ref.cpp -o oracle/_ref/libstbi_ref_pattern.so; \
 	  else echo "ref: $(REF_INC)/stb_image.h not present, skipping oracle/_ref"; fi
 
 kat:

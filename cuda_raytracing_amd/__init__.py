@@ -84,8 +84,8 @@ class World:
         return self._L.rt_mat_lambert_checker(self._w, scale, vec3(*even), vec3(*odd))
 
     def image(self, name: str = "earthmap.jpg") -> _abi.Material:
-        """Image texture from a file (stbi_loadf semantics, load_image); a missing file renders magenta
-        like the reference's failed load, an undecodable one makes status() RT_ERR_UNSUPPORTED."""
+        """Image texture from a file (stbi_loadf semantics, load_image); a missing or undecodable file
+        renders magenta like the reference's failed load; GIF / PSD / PIC make status() RT_ERR_UNSUPPORTED."""
         return self._L.rt_mat_lambert_image(self._w, name.encode())
 
     def status(self) -> int:
@@ -211,9 +211,10 @@ def build_scene(index: int, capacity: int | None = None):
 
 
 def load_image(path: str):
-    """rt_image_load: float32 [H, W, 3] texels (row 0 = top, 8-bit channels as powf(c/255, 2.2)), or None
-    when the file does not exist (the reference's failed load).  RenderError(RT_ERR_UNSUPPORTED) for a
-    format other than binary PNM / BMP / TGA."""
+    """rt_image_load: float32 [H, W, 3] texels as stbi_loadf(path, .., 3) returns them (row 0 = top; JPEG,
+    PNG, BMP, TGA, PNM with 8-bit channels as powf(c/255, 2.2); Radiance HDR as stored), or None when the
+    file does not exist or stb would fail to load it (the reference's failed load: a magenta texture).
+    RenderError(RT_ERR_UNSUPPORTED) for GIF / PSD / PIC files, which this build does not decode."""
     L = _abi.host_lib()
     p = C.POINTER(C.c_float)()
     w, h = C.c_int32(0), C.c_int32(0)

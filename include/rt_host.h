@@ -63,9 +63,10 @@ int32_t rt_world_rand(rt_world *w);
 /* ---- scene builder API (raytracing.cu:1775-1977); materials are returned by value ---- */
 rtr_material rt_mat_lambert_solid(rt_world *w, rtr_vec3 albedo);                 /* :1805 */
 rtr_material rt_mat_light_solid(rt_world *w, rtr_vec3 color);                    /* :1813 */
-/* :1821.  Loads the file like stbi_loadf(file, .., 3) (image_load.cpp: binary PNM, BMP, TGA).  A missing
- * file is the reference's failed load (magenta texture); an existing file in another format sets the
- * world's status to RT_ERR_UNSUPPORTED (rt_world_status, returned by rt_world_build_scene). */
+/* :1821.  Loads the file like stbi_loadf(file, .., 3) (rt_image_load).  A missing, unknown or corrupt file
+ * is the reference's failed load (magenta texture); a GIF / PSD / PIC file, which this build does not
+ * decode, sets the world's status to RT_ERR_UNSUPPORTED (rt_world_status, returned by
+ * rt_world_build_scene). */
 rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name);
 /* an image texture whose load succeeded: width*height float RGB texels (stbi_loadf layout, row 0 first) */
 rtr_material rt_mat_lambert_image_pixels(rt_world *w, const float *rgb, int32_t width, int32_t height);
@@ -90,9 +91,11 @@ int rt_add_pyramid(rt_world *w, int xf, float angle, rtr_vec3 offset,
                    rtr_vec3 base_a, rtr_vec3 base_b, rtr_vec3 tip, rtr_material mat);
 
 /* ---- image files (make_image_texture's stbi_loadf, raytracing.cu:332-341) ----
- * *rgb = width*height float RGB texels, row 0 = top, 8-bit channels as powf(c/255, 2.2) (stb_image's
- * LDR->float rule); free with rt_image_free.  Returns RT_OK, RT_IMAGE_MISSING (no such file: the
- * reference's failed load) or RT_ERR_UNSUPPORTED (a format other than binary PNM / BMP / TGA). */
+ * *rgb = width*height float RGB texels, row 0 = top, as stb_image v2.30's stbi_loadf(path, .., 3) returns
+ * them: JPEG (baseline + progressive), PNG, BMP, TGA, binary PNM with 8-bit channels as powf(c/255, 2.2),
+ * Radiance HDR as stored; free with rt_image_free.  Returns RT_OK, RT_IMAGE_MISSING (no such file, or a
+ * file stb would fail to load: the reference's failed load, a magenta texture) or RT_ERR_UNSUPPORTED (a
+ * GIF, PSD or Softimage PIC file, which stb decodes and this build does not). */
 #define RT_IMAGE_MISSING 1
 int rt_image_load(const char *path, float **rgb, int32_t *width, int32_t *height);
 void rt_image_free(float *rgb);

@@ -1,14 +1,24 @@
 """Image files for image textures (make_image_texture's stbi_loadf, raytracing.cu:332-341), no GPU needed.
 
-rt_image_load decodes binary PNM (P5/P6), BMP (24/32 bit BI_RGB) and TGA (uncompressed 8/24/32 bit) the
-way stbi_loadf(file, .., 3) returns them: float RGB, row 0 = top of the picture, grey replicated, alpha
-dropped, 8-bit channels as powf(c / 255.0f, 2.2f) (stb_image's LDR->float rule).  Expected texels are
-built here from the same picture the file encodes.  The rule's powf is checked against the correctly
-rounded pow of the same float operands (tolerance: 0 ulp).
+rt_image_load returns what stbi_loadf(file, .., 3) (stb_image v2.30, vendored by the reference) returns:
+float RGB, row 0 = top of the picture, grey replicated, alpha dropped, 8-bit channels as
+powf(c / 255.0f, 2.2f), Radiance HDR as stored; a missing, unknown or corrupt file is the reference's failed
+load (None: a magenta texture).  Tolerance everywhere: 0 ulp.
+
+Pinning: the reference's own loader is compiled from /root/reference into oracle/_ref (make ref) as-is and
+twice with its uninitialised memory made explicit (zeros / a pattern: oracle/stbi_ref.cpp).  Every file of
+tests/image_corpus.py (JPEG baseline / progressive / restart / grey / CMYK, PNG of every colour type and bit
+depth, Adam7, all filters and DEFLATE block types, BMP 1-32 bit with bit fields and V4 / V5 / OS/2 headers,
+TGA raw / RLE / colour-mapped / 16-bit, HDR flat / RLE) and thousands of truncated or corrupted copies must
+decode to the same bits as the zero build, and as the as-is build wherever the two explicit builds agree.
+Without /root/reference (the GPU box) the committed fixtures under tests/golden/images pin the same path:
+files plus the SHA-256 of the reference loader's output (tools/gen_image_golden.py).
 """
 from __future__ import annotations
 
 import ctypes as C
+import hashlib
+import json
 import struct
 from pathlib import Path
 
@@ -19,15 +29,29 @@ import cuda_raytracing_amd as rt
 from cuda_raytracing_amd import _abi
 
 
-REF_STBI = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "libstbi_ref.so"
+import image_corpus as corpus
+
+REF_DIR = Path(__file__).resolve().parents[1] / "oracle" / "_ref"
+REF_STBI = REF_DIR / "libstbi_ref.so"
+GOLDEN = Path(__file__).resolve().parent / "golden" / "images"
+_LIBS: dict = {}
+needs_ref = pytest.mark.skipif(not REF_STBI.exists(), reason="oracle/_ref not built (needs /root/reference)")
 
 
-def stbi_loadf(path):
-    """The reference's own loader (stb_image v2.30 compiled where it lies, oracle/stbi_ref.cpp)."""
-    L = C.CDLL(str(REF_STBI))
-    L.rt_ref_stbi_loadf.restype = C.POINTER(C.c_float)
-    L.rt_ref_stbi_loadf.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
-    L.rt_ref_stbi_free.argtypes = [C.c_void_p]
+def _ref_lib(variant: str):
+    if variant not in _LIBS:
+        L = C.CDLL(str(REF_DIR / f"libstbi_ref{variant}.so"))
+        L.rt_ref_stbi_loadf.restype = C.POINTER(C.c_float)
+        L.rt_ref_stbi_loadf.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.rt_ref_stbi_free.argtypes = [C.c_void_p]
+        _LIBS[variant] = L
+    return _LIBS[variant]
+
+
+def stbi_loadf(path, variant: str = ""):
+    """The reference's own loader (stb_image v2.30 compiled where it lies, oracle/stbi_ref.cpp); variant
+    "_zero" / "_pattern": the builds with uninitialised memory set to zeros / a pattern."""
+    L = _ref_lib(variant)
     w, h = C.c_int(0), C.c_int(0)
     p = L.rt_ref_stbi_loadf(str(path).encode(), C.byref(w), C.byref(h))
     if not p:
@@ -36,6 +60,31 @@ def stbi_loadf(path):
         return np.ctypeslib.as_array(p, shape=(h.value, w.value, 3)).copy()
     finally:
         L.rt_ref_stbi_free(p)
+
+
+def load_or_code(path):
+    """rt_image_load through the package: texels, None (failed load) or the error code."""
+    try:
+        return rt.load_image(path)
+    except rt.RenderError as e:
+        return e.code
+
+
+def same(a, b) -> bool:
+    if a is None or b is None or isinstance(a, int) or isinstance(b, int):
+        return (a is None and b is None) or (isinstance(a, int) and a is b)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def agrees_with_reference(path) -> tuple[bool, bool]:
+    """(rt_image_load == the reference loader, the reference's output depends on memory it never wrote).
+    A zero-area image, which stb returns for some corrupt headers, is a failed load here (image_load.cpp)."""
+    got = load_or_code(path)
+    zero, pattern, asis = (stbi_loadf(path, v) for v in ("_zero", "_pattern", ""))
+    if zero is not None and zero.size == 0:
+        zero = pattern = asis = None
+    uninit = not same(zero, pattern)
+    return same(got, zero) and (uninit or same(got, asis)), uninit
 
 
 def check_vs_stb(path, got):
@@ -152,8 +201,22 @@ def test_missing_file_is_the_reference_failed_load(tmp_path):
 
 
 @pytest.mark.parametrize("payload", [b"\xff\xd8\xff\xe0\x00\x10JFIF\x00", b"\x89PNG\r\n\x1a\n\x00\x00", b"P3\n1 1\n255\n0 0 0\n",
-                                     b"P6\n1 1\n65536\n\0\0\0\0\0\0", b"P6\n2 1\n255\n\0\0\0"])
-def test_other_formats_are_unsupported(tmp_path, payload):
+                                     b"P6\n1 1\n65536\n\0\0\0\0\0\0", b"", b"hello world", b"BM\0\0"])
+def test_corrupt_and_unknown_files_are_the_reference_failed_load(tmp_path, payload):
+    # stbi_loadf returns NULL: the texture renders magenta, the world stays valid
+    f = tmp_path / "earthmap.jpg"
+    f.write_bytes(payload)
+    assert rt.load_image(f) is None
+    check_vs_stb(f, None)
+    w = rt.World()
+    m = w.image(str(f))
+    assert w.status() == 0 and m.kind == 0
+
+
+@pytest.mark.parametrize("payload", [b"GIF89a\x01\x00\x01\x00\x00\x00\x00;", b"8BPS\x00\x01" + b"\0" * 30,
+                                     b"\x53\x80\xF6\x34" + b"\0" * 84 + b"PICT" + b"\0" * 16])
+def test_formats_this_build_does_not_decode_are_unsupported(tmp_path, payload):
+    # GIF, PSD and Softimage PIC: stb would decode them; this build says so loudly instead of guessing
     f = tmp_path / "earthmap.jpg"
     f.write_bytes(payload)
     with pytest.raises(rt.RenderError) as e:
@@ -166,23 +229,28 @@ def test_other_formats_are_unsupported(tmp_path, payload):
 
 def test_earth_scene_loads_its_texture(tmp_path, monkeypatch, picture):
     # the catalog's earth scene (raytracing.cu:2042-2052) names earthmap.jpg relative to the working
-    # directory: absent -> magenta texture (the reference's run), a JPEG -> unsupported, and the texels
-    # of a decodable file end up in the texture arena behind the image Texture record (:270-279)
+    # directory: absent or corrupt -> magenta texture (the reference's run), and the texels of a
+    # decodable file (a real JPEG here) end up in the texture arena behind the image Texture record
+    # (:270-279)
     monkeypatch.chdir(tmp_path)
     idx = [rt.scene_name(i) for i in range(rt.RT_SCENE_COUNT)].index("earth")
     w = rt.World()
     w.build_scene(idx)
     assert w.status() == 0
     (tmp_path / "earthmap.jpg").write_bytes(b"\xff\xd8\xff\xe0")
-    with pytest.raises(rt.RenderError):
-        rt.World().build_scene(idx)
-    (tmp_path / "earthmap.jpg").write_bytes(b"P6 7 5 255\n" + picture.tobytes())
+    w1 = rt.World()
+    w1.build_scene(idx)
+    assert w1.status() == 0
+    pic = corpus.picture(64, 128, seed=3)
+    (tmp_path / "earthmap.jpg").write_bytes(corpus.pil_bytes(pic, "JPEG", quality=90))
+    texels = rt.load_image(tmp_path / "earthmap.jpg")
+    check_vs_stb(tmp_path / "earthmap.jpg", texels)
+    assert texels.shape == (64, 128, 3)
     w2 = rt.World()
     w2.build_scene(idx)
     sc = w2.scene()
     arena = np.frombuffer(C.string_at(sc.textures, sc.texture_bytes), np.uint8)
-    want = expect(picture).tobytes()
-    assert arena.tobytes().find(want) > 0
+    assert arena.tobytes().find(texels.tobytes()) > 0
 
 
 @pytest.mark.skipif(not REF_STBI.exists(), reason="oracle/_ref not built (needs /root/reference)")
@@ -203,3 +271,96 @@ def test_reference_loader_is_pinned_on_random_images(tmp_path):
             got = rt.load_image(f)
             ref = stbi_loadf(f)
             assert ref is not None and np.array_equal(ref.view(np.uint32), got.view(np.uint32)), f
+
+
+# ---------------------------------------------------------------- every format stb reads
+
+CORPUS_SIZES = [(1, 1), (2, 3), (8, 8), (16, 17), (37, 53), (3, 200), (70, 9)]
+
+
+@needs_ref
+@pytest.mark.parametrize("size", CORPUS_SIZES, ids=lambda s: f"{s[0]}x{s[1]}")
+def test_corpus_matches_the_reference_loader(tmp_path, size):
+    files = corpus.corpus(CORPUS_SIZES.index(size), *size)
+    assert len(files) >= 90
+    bad = []
+    for name, data in files.items():
+        f = tmp_path / name
+        f.write_bytes(data)
+        ok, _ = agrees_with_reference(f)
+        if not ok:
+            bad.append(name)
+    assert not bad, bad
+
+
+@needs_ref
+@pytest.mark.parametrize("seed", [1, 2])
+def test_truncated_and_corrupted_files_match_the_reference_loader(tmp_path, seed):
+    # truncations, random byte stores, bit flips in the headers and random runs, over the whole corpus:
+    # success / failure and every texel as the reference loader (its zero build where it reads memory
+    # it never wrote — rt_image_load reads zeros there)
+    rng = np.random.default_rng(seed)
+    files = corpus.corpus(seed, int(rng.integers(1, 40)), int(rng.integers(1, 60)))
+    bad, n, uninit = [], 0, 0
+    for name, data in files.items():
+        for trial in range(8):
+            d = bytearray(data)
+            kind = trial % 4
+            if kind == 0:
+                d = d[:int(rng.integers(0, len(d)))]
+            elif kind == 1:
+                for _ in range(int(rng.integers(1, 4))):
+                    d[int(rng.integers(0, len(d)))] = int(rng.integers(0, 256))
+            elif kind == 2:
+                d[int(rng.integers(0, min(len(d), 300)))] ^= 1 << int(rng.integers(0, 8))
+            else:
+                i = int(rng.integers(0, len(d)))
+                j = min(len(d), i + int(rng.integers(1, 64)))
+                d[i:j] = rng.integers(0, 256, j - i, dtype=np.uint8).tobytes()
+            f = tmp_path / ("x." + name.rsplit(".", 1)[1])
+            f.write_bytes(bytes(d))
+            ok, u = agrees_with_reference(f)
+            n += 1
+            uninit += u
+            if not ok:
+                bad.append((name, trial))
+    assert n >= 800 and not bad, bad
+
+
+def test_hdr_texels_are_the_stored_rgbe_values(tmp_path):
+    # independent of stb: mantissa * 2^(exponent - 136), a zero exponent is black; flat and RLE scanlines
+    for seed, rle, (h, w) in [(0, False, (6, 5)), (1, True, (9, 40)), (2, True, (3, 9))]:
+        rgbe = corpus._rgbe(h, w, seed)
+        f = tmp_path / f"{seed}.hdr"
+        f.write_bytes(corpus.hdr_bytes(rgbe, rle))
+        got = rt.load_image(f)
+        check_vs_stb(f, got)
+        want = corpus.hdr_expected(rgbe)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+        assert got[0, 0].tolist() == [0.0, 0.0, 0.0]
+
+
+def test_png_and_bmp_decode_the_picture_they_encode(tmp_path):
+    # independent of stb: lossless formats give back the picture they were written from
+    pic = corpus.picture(13, 21, seed=9, smooth=False)
+    cases = {"a.png": corpus.png_bytes(pic, 2, 8, interlace=True), "b.png": corpus.png_bytes(pic, 2, 8, level=0),
+             "c.bmp": corpus.bmp_variants(pic)["v5_24.bmp"], "d.bmp": corpus.bmp_variants(pic)["os2_24.bmp"]}
+    for name, data in cases.items():
+        f = tmp_path / name
+        f.write_bytes(data)
+        got = rt.load_image(f)
+        assert np.array_equal(got.view(np.uint32), expect(pic).view(np.uint32)), name
+
+
+def test_golden_fixtures(tmp_path):
+    # committed files + the SHA-256 of the reference loader's float texels (tools/gen_image_golden.py):
+    # pins the decoders where /root/reference is absent (the GPU box)
+    manifest = json.loads((GOLDEN / "manifest.json").read_text())
+    assert len(manifest) >= 12
+    for name, want in manifest.items():
+        got = rt.load_image(GOLDEN / name)
+        if want is None:
+            assert got is None, name
+            continue
+        assert list(got.shape) == want["shape"], name
+        assert hashlib.sha256(np.ascontiguousarray(got, np.float32).tobytes()).hexdigest() == want["sha256"], name
