@@ -69,6 +69,25 @@ def op_model(counters: dict, samples: int) -> float:
     return ops / max(samples, 1)
 
 
+# the verified SAH walk of all-sphere worlds (AccelTraceK): per executed node visit two child boxes of the
+# reference's slab test (2 x visit_bvh), per leaf test one sphere test (visit_sphere)
+EXEC_NODE_OPS = 2 * OP_WEIGHTS["visit_bvh"]
+EXEC_PRIM_OPS = OP_WEIGHTS["visit_sphere"]
+
+
+def executed_op_model(counters: dict, samples: int):
+    """Ops per sample of the work the verified walk EXECUTES (its node visits and leaf tests, counted by the
+    counting variant, exec_node / exec_prim) in place of the reference walk's BVH and sphere visits; None
+    when the workload does not take that walk.  The headline frac keeps the reference's visits (the same
+    op model in every round); this second frac says how busy the VALU is on the work actually done."""
+    if not counters.get("exec_node"):
+        return None
+    ops = op_model(counters, samples) * max(samples, 1)
+    ops -= OP_WEIGHTS["visit_bvh"] * counters["visit_bvh"] + OP_WEIGHTS["visit_sphere"] * counters["visit_sphere"]
+    ops += EXEC_NODE_OPS * counters["exec_node"] + EXEC_PRIM_OPS * counters["exec_prim"]
+    return ops / max(samples, 1)
+
+
 def cpu_model() -> str:
     try:
         for line in Path("/proc/cpuinfo").read_text().splitlines():
@@ -234,13 +253,15 @@ def e2e_cli(scene: int, W: int, H: int, spp: int, bounces: int):
     return res
 
 
-def load_traffic(workload: str):
+def load_traffic(workload: str, key: str = "bytes"):
+    """PMC HBM bytes per launch of the render kernel ("bytes") or of the whole step ("step_bytes": seeding,
+    probe, tile order, render), from profiles/hbm_traffic.json (tools/traffic_from_pmc.py)."""
     f = REPO / "profiles" / "hbm_traffic.json"
     if not f.exists():
         return None
     try:
         d = json.loads(f.read_text()).get(workload)
-        return int(d["bytes"]) if d else None
+        return int(d[key]) if d and key in d else None
     except Exception:
         return None
 
@@ -368,6 +389,7 @@ def main():
     seed_ms = med([st.init_ms for st in fstats])
     sched_ms = med([st.sched_ms for st in fstats])
     achieved = ops_per_sample * local_samples / (render_ms / 1e3) / 1e12
+    exec_ops = executed_op_model(counters, counters["samples"])
 
     # ---- secondary: two frames in flight (independent frames overlap their tails) ----
     psteps = args.steps if args.pipelined_steps < 0 else args.pipelined_steps
@@ -441,7 +463,13 @@ def main():
                 "unit": "Tops/s",
                 "frac": round(achieved / VALU_PEAK_TOPS, 4),
                 "traffic": load_traffic(workload),
+                "step_traffic": load_traffic(workload, "step_bytes"),
                 "ops_per_sample": round(ops_per_sample, 1),
+                "executed": None if exec_ops is None else {
+                    "ops_per_sample": round(exec_ops, 1),
+                    "frac": round(exec_ops * local_samples / (render_ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 4),
+                    "note": "verified SAH walk's executed node visits (2 boxes each) and leaf tests instead of the "
+                            "reference tree's visits"},
                 "measured_on": "median render-kernel HIP-event duration over the timed frames (launch stream)",
                 "counters_per_sample": {k: round(v / max(counters["samples"], 1), 4) for k, v in counters.items()
                                         if k not in ("samples", "max_stack", "stack_overflow", "rng_draws")},

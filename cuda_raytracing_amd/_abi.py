@@ -37,7 +37,7 @@ RT_TRAV_LANE, RT_TRAV_PACKET, RT_TRAV_STATIC, RT_TRAV_ACCEL, RT_TRAV_MIXED = 0, 
 CNT_NAMES = [
     "visit_sphere", "visit_bvh", "visit_triangle", "visit_quad", "visit_translate",
     "visit_yrotate", "visit_group", "bounces", "shades", "perlin", "rng_draws", "samples",
-    "max_stack", "stack_overflow", "reserved14", "reserved15",
+    "max_stack", "stack_overflow", "exec_node", "exec_prim",
 ]
 
 RT_XF_NONE, RT_XF_TRANSLATE, RT_XF_YROTATE, RT_XF_YROTATE_TRANSLATE = 0, 1, 2, 3

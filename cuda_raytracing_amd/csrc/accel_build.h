@@ -159,6 +159,36 @@ struct Builder {
     w[15] = fb(up(rm));
     return idx;
   }
+
+  // renumber the internal nodes breadth-first from `root` (which becomes node 0), so that the top levels
+  // of the tree are the first nodes: a prefix of the array is a complete top of the tree (the part a
+  // kernel can stage in LDS); leaf references are unchanged
+  uint32_t bfs_order(uint32_t root) {
+    const uint32_t count = static_cast<uint32_t>(nodes.size() / kAccelNodeWords);
+    std::vector<uint32_t> order_bfs, new_id(count, 0xffffffffu);
+    order_bfs.reserve(count);
+    order_bfs.push_back(root);
+    new_id[root] = 0;
+    for (size_t i = 0; i < order_bfs.size(); ++i) {
+      const uint32_t *w = &nodes[static_cast<size_t>(order_bfs[i]) * kAccelNodeWords];
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t ch = w[12 + c];
+        if (ch & kAccelLeaf) continue;
+        new_id[ch] = static_cast<uint32_t>(order_bfs.size());
+        order_bfs.push_back(ch);
+      }
+    }
+    std::vector<uint32_t> out(nodes.size());
+    for (size_t i = 0; i < order_bfs.size(); ++i) {
+      uint32_t *o = &out[i * kAccelNodeWords];
+      std::memcpy(o, &nodes[static_cast<size_t>(order_bfs[i]) * kAccelNodeWords], kAccelNodeWords * 4);
+      for (int c = 0; c < 2; ++c)
+        if (!(o[12 + c] & kAccelLeaf)) o[12 + c] = new_id[o[12 + c]];
+    }
+    out.resize(order_bfs.size() * kAccelNodeWords);
+    nodes.swap(out);
+    return 0;
+  }
 };
 
 }  // namespace accel

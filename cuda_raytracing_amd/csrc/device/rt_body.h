@@ -17,6 +17,9 @@
 #ifndef RT_UNWIND_LDS
 #define RT_UNWIND_LDS 3     // LDS colour-stack levels loaded per batch in the unwind
 #endif
+#ifndef RT_ACCEL_EARLY_NEXT
+#define RT_ACCEL_EARLY_NEXT 0   // verified sphere walk: fetch the next node before the leaf tests (A/B knob)
+#endif
 #ifndef RT_UNWIND_LDS_DEEP
 #define RT_UNWIND_LDS_DEEP 8   // ... in deep-path kernels (max_bounces > kDeepBounces)
 #endif
@@ -443,7 +446,7 @@ struct Ray { f3 o, d; float time; };
 struct Hit { f3 p, n; float t, u, v, fd; uint32_t mat; };
 __device__ __forceinline__ bool hit_front(const Hit &h) { return h.fd < 0.0f; }
 __device__ __forceinline__ f3 hit_normal(const Hit &h) { return hit_front(h) ? h.n : flip(h.n); }
-struct Visits { uint32_t k[7]; uint32_t max_sp; };
+struct Visits { uint32_t k[7]; uint32_t max_sp; uint32_t xn, xp; };   // xn / xp: executed SAH node visits / leaf tests
 
 // locals of hit() (:1082-1088) plus a cached 1/dir
 struct Trav {
@@ -885,7 +888,12 @@ struct AccelTraceK {
     // (and 2|d|^2 >= 2^-40, so that the roots' division by 2a can use the ray's reciprocal, sphere_hit_tie)
     // (and max |d_i| >= 7e-7, so 2|d|^2 >= 2^-40 and the roots' division by 2a can use the ray's
     // reciprocal, sphere_hit_tie)
-    const bool nice = !COUNT && (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f) && (dmax >= 7.0e-7f);
+    // The counting variant runs the walk on copies (never pausing) only to count its executed node visits
+    // and leaf tests (vc.xn / vc.xp: the op model's second, executed-work frac), then walks the
+    // reference tree for the record so that the op model also counts the reference's visits.
+    bool nice = (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f) && (dmax >= 7.0e-7f);
+    const Trav tsave = T;
+    const Hit hsave = h;
     bool tie = resume && T.atie != 0;
     uint32_t best = resume ? T.abest : 0u;
     const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
@@ -906,9 +914,25 @@ struct AccelTraceK {
       // steps); those lanes keep node, stack and best hit and resume next round, skipping shading
       // meanwhile.  A walk's steps and order are unchanged, so the record is the same.
       const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(walking)));
+      // the top of the tree from LDS (A.accel_lds_nodes breadth-first nodes), the rest from HBM / L2
+      // (two explicit loads rather than one generic pointer: flat loads would wait on both counters)
+      uint4 q0, q1, q2, q3;
+      auto load_node = [&](uint32_t nd) {
+        if (nd < A.accel_lds_nodes) {
+          const uint4 *L = reinterpret_cast<const uint4 *>(g_lds);
+          q0 = L[nd * 4]; q1 = L[nd * 4 + 1]; q2 = L[nd * 4 + 2]; q3 = L[nd * 4 + 3];
+        } else {
+          q0 = N[nd * 4]; q1 = N[nd * 4 + 1]; q2 = N[nd * 4 + 2]; q3 = N[nd * 4 + 3];
+        }
+      };
+      // RT_ACCEL_EARLY_NEXT: the next node is chosen before the leaf tests (they change tmax, not the
+      // order) and its data fetched under them
+      constexpr bool EARLY = RT_ACCEL_EARLY_NEXT != 0;
+      if (EARLY && walking) load_node(node);
       for (uint32_t it = 1;; ++it) {
         if (walking) {
-        const uint4 q0 = N[node * 4], q1 = N[node * 4 + 1], q2 = N[node * 4 + 2], q3 = N[node * 4 + 3];
+        if (!EARLY) load_node(node);
+        if (COUNT) vc.xn++;
         float n0, n1;
         bool h0 = accel_box(T, sr, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), &n0);
         bool h1 = accel_box(T, sr, asf(q1.z), asf(q1.w), asf(q2.x), asf(q2.y), asf(q2.z), asf(q2.w), &n1);
@@ -920,32 +944,40 @@ struct AccelTraceK {
         const bool ln = hn && (rn & kAccelLeaf), lf = hf && (rf & kAccelLeaf);
         const uint32_t c1 = ln ? ((rn >> 24) & 0x7fu) + 1u : 0u, c2 = lf ? ((rf >> 24) & 0x7fu) + 1u : 0u;
         const uint32_t f1 = rn & 0xffffffu, f2 = (rf & 0xffffffu) - c1;
+        hn = hn && !ln;
+        hf = hf && !lf;
+        auto next_node = [&]() {
+          if (hn && hf) {
+            stk[sp * 64] = static_cast<uint16_t>(rf);
+            ++sp;
+            node = rn;
+          } else if (hn | hf) {
+            node = hn ? rn : rf;
+          } else if (sp == 0) {
+            walking = false;
+          } else {
+            --sp;
+            node = stk[sp * 64];
+          }
+        };
+        if (EARLY) {
+          next_node();
+          if (walking) load_node(node);
+        }
         for (uint32_t k = 0; k < c1 + c2; ++k) {
           const uint32_t pr = (k < c1 ? f1 : f2) + k;
+          if (COUNT) vc.xp++;
           const uint4 p0 = P[pr * 4], p1 = P[pr * 4 + 1], p2 = P[pr * 4 + 2];
           if (sphere_hit_tie<UV, true, false>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)),
                                        asf(p1.z), asf(p1.w), sa2, sra2, tie))
             best = pr;
         }
-        hn = hn && !ln;
-        hf = hf && !lf;
-        if (hn && hf) {
-          stk[sp * 64] = static_cast<uint16_t>(rf);
-          ++sp;
-          node = rn;
-        } else if (hn | hf) {
-          node = hn ? rn : rf;
-        } else if (sp == 0) {
-          walking = false;
-        } else {
-          --sp;
-          node = stk[sp * 64];
-        }
+        if (!EARLY) next_node();
         }
         const uint64_t left = __ballot(walking);
         if (left == 0) break;
         const uint32_t nl = static_cast<uint32_t>(__popcll(left));
-        if (it >= A.trace_min_iters && nl <= A.defer_trace && 4 * nl <= started) break;
+        if (!COUNT && it >= A.trace_min_iters && nl <= A.defer_trace && 4 * nl <= started) break;
       }
       if (walking) {   // paused: resume next round
         T.active = 1; T.anode = node; T.asp = sp; T.abest = best; T.atie = tie ? 1u : 0u;
@@ -953,6 +985,11 @@ struct AccelTraceK {
       }
     }
     T.active = 0;
+    if (COUNT) {   // counted; the record comes from the reference walk below
+      T = tsave;
+      h = hsave;
+      nice = false;
+    }
     bool need_ref = !nice || tie;
     if (nice && T.result) {
       const uint4 p0 = P[best * 4], p1 = P[best * 4 + 1], p2 = P[best * 4 + 2];
@@ -1477,6 +1514,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
     for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
     __syncthreads();
+  } else if (A.accel_lds_nodes) {   // the verified walk's top nodes (4 uint4 each)
+    const uint4 *src = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
+    uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
+    for (uint32_t i = threadIdx.x; i < A.accel_lds_nodes * 4; i += kBlock) dst[i] = src[i];
+    __syncthreads();
   }
   const uint32_t lane = __lane_id();
   const uint32_t wave = threadIdx.x >> 6;
@@ -1945,6 +1987,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};
     for (int k = 0; k < 7; ++k) vals[k] = vc.k[k];
+    vals[CNT_EXEC_NODE] = vc.xn;
+    vals[CNT_EXEC_PRIM] = vc.xp;
     vals[CNT_BOUNCES] = c_bounce;
     vals[CNT_SHADES] = c_shade;
     vals[CNT_PERLIN] = c_perlin;

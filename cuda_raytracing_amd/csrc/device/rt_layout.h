@@ -100,7 +100,7 @@ constexpr int kPerlinPermWord = 256 * 4, kPerlinPerm2Word = 256 * 4 + 64;
 // counter slots == RT_CNT_* (rt_render.h)
 enum : int {
   CNT_VISIT0 = 0, CNT_BOUNCES = 7, CNT_SHADES = 8, CNT_PERLIN = 9, CNT_RNG = 10, CNT_SAMPLES = 11,
-  CNT_MAX_STACK = 12, CNT_OVERFLOW = 13, CNT_SLOTS = 16
+  CNT_MAX_STACK = 12, CNT_OVERFLOW = 13, CNT_EXEC_NODE = 14, CNT_EXEC_PRIM = 15, CNT_SLOTS = 16
 };
 
 constexpr int kBlock = 256;        // 4 waves of 64
@@ -184,6 +184,7 @@ struct RenderArgs {
   uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
   uint32_t accel_nodes, accel_prims, accel_root;   // verified sphere traversal (word offsets, root node)
+  uint32_t accel_lds_nodes;       // its first nodes (breadth-first: the top levels) staged at LDS word 0
   uint32_t *accel_fallbacks;      // rays the verified traversal handed to the reference walk (diagnostic)
   uint32_t defer_trace;           // verified traversal: the round's walk stops once at most this many
   uint32_t trace_min_iters;       // lanes (and <= 1/4 of the starters) still walk, after this many steps

@@ -143,6 +143,7 @@ struct rt_context {
   rt::SphereAccel accel;
   bool accel_ok = false;
   uint32_t accel_nodes = 0, accel_prims = 0;   // word offsets in the device image
+  uint32_t accel_lds_nodes = 0;                 // top SAH nodes staged in LDS (RT_ACCEL_LDS_NODES)
   // verified mixed-world traversal (RT_TRAV_MIXED): macro roots marked in the image, SAH words appended
   rt::MixedAccel mixed;
   bool mixed_ok = false;
@@ -306,6 +307,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_MIX_PROVE")) c->mix_no_proof = e[0] == '0';
+  if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
@@ -530,6 +532,14 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   }
   if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
   if (jit_fn && !jit_lane) stack_bytes = 0;   // straight-line traversal: no stacks
+  // the verified walk's top nodes staged in LDS (breadth-first prefix of the SAH tree) where the scene
+  // itself is not: they take the scene's place at the start of the block's LDS
+  uint32_t accel_lds_nodes = 0;
+  if (trav == RT_TRAV_ACCEL && !c->lds && c->accel_lds_nodes > 0) {
+    accel_lds_nodes = std::min<uint32_t>(c->accel_lds_nodes,
+                                         static_cast<uint32_t>(c->accel.node_words.size() / rt::kAccelNodeWords));
+    scene_lds_words = accel_lds_nodes * rt::kAccelNodeWords;
+  }
   const bool narrow = jit_fn != nullptr && narrow_ok;   // the offline kernels use 32-bit codes
   const size_t level_bytes = rc_level_bytes(narrow);
   if (narrow) rc_levels = (rc_levels + 1) & ~1u;        // two levels per LDS word
@@ -601,6 +611,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.accel_nodes = c->accel_nodes;
   a.accel_prims = c->accel_prims;
   a.accel_root = c->accel.root;
+  a.accel_lds_nodes = accel_lds_nodes;
   a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
   a.mix_nodes = c->mix_nodes;
   a.mix_prims = c->mix_prims;

@@ -107,8 +107,11 @@ bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel
   bd.prims = std::move(prims);
   Box rb;
   double rm;
-  const uint32_t root = bd.build(0, static_cast<uint32_t>(bd.prims.size()), 1, &rb, &rm);
+  uint32_t root = bd.build(0, static_cast<uint32_t>(bd.prims.size()), 1, &rb, &rm);
   if (root & kAccelLeaf) { if (why) *why = "degenerate tree"; return false; }
+  // breadth-first node order (the top levels first: what RT_ACCEL_LDS_NODES stages in LDS);
+  // RT_ACCEL_BFS=0 keeps the builder's depth-first order
+  if (!(std::getenv("RT_ACCEL_BFS") && std::getenv("RT_ACCEL_BFS")[0] == '0')) root = bd.bfs_order(root);
   if (bd.nodes.size() / kAccelNodeWords >= 65536) { if (why) *why = "tree too large for u16 stack entries"; return false; }
   out->root = root;
   out->depth = bd.max_depth;

@@ -109,6 +109,8 @@ enum {
   RT_CNT_SAMPLES,
   RT_CNT_MAX_STACK,        /* deepest hit-stack use seen (max, not sum) */
   RT_CNT_STACK_OVERFLOW,   /* traversals that would have overflowed (must be 0) */
+  RT_CNT_EXEC_NODE,        /* verified SAH walk (all-sphere worlds): node visits it executes (2 child boxes each) */
+  RT_CNT_EXEC_PRIM,        /* verified SAH walk: leaf spheres it tests */
   RT_CNT__COUNT = 16
 };
 

@@ -315,18 +315,14 @@ def test_image_texture_scene_vs_oracle():
 
 
 def test_earth_scene_with_a_texture_file_vs_oracle(tmp_path, monkeypatch):
-    # the catalog's earth scene (raytracing.cu:2042-2052) with an earthmap file this build decodes (a
-    # 24-bit BMP written here; the reference's JPEG is absent): texels loaded like stbi_loadf, rendered
-    # on the GPU and by the oracle from the same arena bytes
-    import struct
-    rng = np.random.default_rng(3)
-    h, w_ = 32, 64
-    pic = rng.integers(0, 256, size=(h, w_, 3), dtype=np.uint8)
-    stride = (w_ * 3 + 3) & ~3
-    rows = b"".join(pic[y, :, ::-1].tobytes() + b"\0" * (stride - 3 * w_) for y in range(h - 1, -1, -1))
-    bmp = struct.pack("<2sIHHI", b"BM", 54 + len(rows), 0, 0, 54) + \
-        struct.pack("<IiiHHIIiiII", 40, w_, h, 1, 24, 0, len(rows), 0, 0, 0, 0) + rows
-    (tmp_path / "earthmap.jpg").write_bytes(bmp)   # the scene's file name; the loader reads the BMP magic
+    # the catalog's earth scene (raytracing.cu:2042-2052) with an earthmap.jpg present (the reference
+    # repository does not ship one): a progressive 4:2:0 JPEG written here, decoded like stbi_loadf
+    # (tests/test_image_load.py pins that against stb itself), rendered on the GPU and by the oracle from
+    # the same arena bytes
+    import image_corpus
+    pic = image_corpus.picture(64, 128, seed=3)
+    (tmp_path / "earthmap.jpg").write_bytes(image_corpus.pil_bytes(pic, "JPEG", quality=85, progressive=True,
+                                                                   subsampling=2))
     monkeypatch.chdir(tmp_path)
     idx = [rt.scene_name(i) for i in range(rt.RT_SCENE_COUNT)].index("earth")
     w, s = rt.build_scene(idx)
