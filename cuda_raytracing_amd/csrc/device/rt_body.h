@@ -17,9 +17,6 @@
 #ifndef RT_UNWIND_LDS
 #define RT_UNWIND_LDS 3     // LDS colour-stack levels loaded per batch in the unwind
 #endif
-#ifndef RT_ACCEL_EARLY_NEXT
-#define RT_ACCEL_EARLY_NEXT 0   // verified sphere walk: fetch the next node before the leaf tests (A/B knob)
-#endif
 #ifndef RT_UNWIND_LDS_DEEP
 #define RT_UNWIND_LDS_DEEP 8   // ... in deep-path kernels (max_bounces > kDeepBounces)
 #endif
@@ -925,13 +922,9 @@ struct AccelTraceK {
           q0 = N[nd * 4]; q1 = N[nd * 4 + 1]; q2 = N[nd * 4 + 2]; q3 = N[nd * 4 + 3];
         }
       };
-      // RT_ACCEL_EARLY_NEXT: the next node is chosen before the leaf tests (they change tmax, not the
-      // order) and its data fetched under them
-      constexpr bool EARLY = RT_ACCEL_EARLY_NEXT != 0;
-      if (EARLY && walking) load_node(node);
       for (uint32_t it = 1;; ++it) {
         if (walking) {
-        if (!EARLY) load_node(node);
+        load_node(node);
         if (COUNT) vc.xn++;
         float n0, n1;
         bool h0 = accel_box(T, sr, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), &n0);
@@ -944,26 +937,6 @@ struct AccelTraceK {
         const bool ln = hn && (rn & kAccelLeaf), lf = hf && (rf & kAccelLeaf);
         const uint32_t c1 = ln ? ((rn >> 24) & 0x7fu) + 1u : 0u, c2 = lf ? ((rf >> 24) & 0x7fu) + 1u : 0u;
         const uint32_t f1 = rn & 0xffffffu, f2 = (rf & 0xffffffu) - c1;
-        hn = hn && !ln;
-        hf = hf && !lf;
-        auto next_node = [&]() {
-          if (hn && hf) {
-            stk[sp * 64] = static_cast<uint16_t>(rf);
-            ++sp;
-            node = rn;
-          } else if (hn | hf) {
-            node = hn ? rn : rf;
-          } else if (sp == 0) {
-            walking = false;
-          } else {
-            --sp;
-            node = stk[sp * 64];
-          }
-        };
-        if (EARLY) {
-          next_node();
-          if (walking) load_node(node);
-        }
         for (uint32_t k = 0; k < c1 + c2; ++k) {
           const uint32_t pr = (k < c1 ? f1 : f2) + k;
           if (COUNT) vc.xp++;
@@ -972,7 +945,20 @@ struct AccelTraceK {
                                        asf(p1.z), asf(p1.w), sa2, sra2, tie))
             best = pr;
         }
-        if (!EARLY) next_node();
+        hn = hn && !ln;
+        hf = hf && !lf;
+        if (hn && hf) {
+          stk[sp * 64] = static_cast<uint16_t>(rf);
+          ++sp;
+          node = rn;
+        } else if (hn | hf) {
+          node = hn ? rn : rf;
+        } else if (sp == 0) {
+          walking = false;
+        } else {
+          --sp;
+          node = stk[sp * 64];
+        }
         }
         const uint64_t left = __ballot(walking);
         if (left == 0) break;
@@ -1583,6 +1569,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool probe_end = false;                  // probe: the lane's path ended in the last round
   uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, ph_unwind = 0, ph_cam = 0, t_mark = 0;   // wave-trace clocks
   uint64_t busy_lane_rounds = 0;
+  uint64_t lph[7] = {0, 0, 0, 0, 0, 0, 0}, lone_rounds = 0;   // wave trace: the same phases over the rounds
+  bool lone = false;                                         // with at most 2 busy lanes (the frame's tail)
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
 
   f3 pp = mk(0, 0, 0);   // the pixel's viewport point (:1565-1567), computed once per pixel
@@ -1624,7 +1612,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   for (;;) {
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
-      if (t_mark) ph_shade += t - t_mark;
+      if (t_mark) { ph_shade += t - t_mark; if (lone) lph[2] += t - t_mark; }
       t_mark = t;
     }
     if (probe) {
@@ -1646,21 +1634,33 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     // ---- lanes without a pixel take the next pixels of the wave's tile ----
     bool need = !busy;
     uint64_t m = __ballot(need);
+    // sparse hot waves (A.prio_lanes < 64, split hand-out only): a wave holding pixels of the costliest
+    // tiles takes at most prio_lanes of them and no other pixel until they are done, so the longest pixel
+    // chains run in waves with few divergent lanes (the idle lanes share their noise octaves)
+    const bool sparse = A.prio_lanes < static_cast<uint32_t>(kChunk);
+    uint32_t nhot = sparse ? static_cast<uint32_t>(__popcll(__ballot(busy && hot))) : 0u;
     while (m != 0 && !exhausted) {
       if (chunk_pos >= chunk_end) {
+        if (sparse && (nhot >= A.prio_lanes || (nhot > 0 && prio_done))) break;
         // the costliest tiles (the first prio_ids ids of the longest-first order) may be handed out in
         // prio_chunk-pixel pieces from their own counter, so that their long pixel chains spread over
         // more waves; every other tile goes out whole
-        uint32_t base = 0, size = static_cast<uint32_t>(kChunk);
+        uint32_t base = 0, size = static_cast<uint32_t>(kChunk), hold = 0;
         const bool split = A.prio_chunk < static_cast<uint32_t>(kChunk) && !prio_done;
         if (lane == 0) {
           if (split) base = atomicAdd(A.work + 1, A.prio_chunk);
-          if (!split || base >= A.prio_ids) base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
-          else size = A.prio_chunk;
+          if (!split || base >= A.prio_ids) {
+            if (sparse && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
+            else base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
+          } else {
+            size = A.prio_chunk;
+          }
         }
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         size = __builtin_amdgcn_readfirstlane(__shfl(size, 0));
+        hold = __builtin_amdgcn_readfirstlane(__shfl(hold, 0));
         if (size == static_cast<uint32_t>(kChunk)) prio_done = true;
+        if (hold) break;
         if (base >= A.n_ids) { exhausted = true; break; }
         if (A.reverse_tiles) base = A.n_ids - kChunk - base;   // whole tiles: n_ids is a multiple of 64
         tiles_taken++;
@@ -1711,6 +1711,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       chunk_pos += min(static_cast<uint32_t>(__popcll(m)), avail);
       m = __ballot(need);
+      if (sparse) nhot = static_cast<uint32_t>(__popcll(__ballot(busy && hot)));
     }
     const uint64_t lanes = __ballot(busy);
     if (lanes == 0) break;   // queue exhausted and every lane idle
@@ -1725,8 +1726,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     rounds++;
     busy_lane_rounds += static_cast<uint64_t>(__popcll(lanes));
     if (TRACE) {
+      lone = __popcll(lanes) <= 2;
+      lone_rounds += lone ? 1u : 0u;
+    }
+    if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
-      ph_refill += t - t_mark;
+      ph_refill += t - t_mark; if (lone) lph[0] += t - t_mark;
       t_mark = t;
     }
 
@@ -1736,7 +1741,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     if (T.active) continue;                   // walk paused (verified traversal): resumes next round
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
-      ph_trace += t - t_mark;
+      ph_trace += t - t_mark; if (lone) lph[1] += t - t_mark;
       t_mark = t;
     }
     // ---- shade (ray_color loop body, :1340-1359); in noise kernels lanes without a pixel stay to help
@@ -1789,7 +1794,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
-      ph_rej += t - t_mark;
+      ph_rej += t - t_mark; if (lone) lph[4] += t - t_mark;
       t_mark = t;
     }
     // ---- cooperative noise (kernels with noise textures): a lane shading a Lambertian noise texture
@@ -1892,7 +1897,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
-      ph_mat += t - t_mark;
+      ph_mat += t - t_mark; if (lone) lph[3] += t - t_mark;
       t_mark = t;
     }
     if (done) {
@@ -1941,7 +1946,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       if (TRACE) {   // the unwind's share of the done block (the rest: camera ray / pixel write)
         const uint64_t t = __builtin_amdgcn_s_memtime();
-        ph_unwind += t - t_mark;
+        ph_unwind += t - t_mark; if (lone) lph[5] += t - t_mark;
         t_mark = t;
       }
       sum = add(sum, res);
@@ -1968,7 +1973,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       if (TRACE) {
         const uint64_t t = __builtin_amdgcn_s_memtime();
-        ph_cam += t - t_mark;
+        ph_cam += t - t_mark; if (lone) lph[6] += t - t_mark;
         t_mark = t;
       }
     }
@@ -1983,6 +1988,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     w[4] = rounds; w[5] = busy_lane_rounds;
     w[6] = ph_refill; w[7] = ph_trace; w[8] = ph_shade; w[9] = ph_mat; w[10] = ph_rej; w[11] = ph_unwind;
     w[12] = ph_cam;
+    w[13] = lone_rounds;
+    for (int k = 0; k < 7; ++k) w[14 + k] = lph[k];
   }
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};

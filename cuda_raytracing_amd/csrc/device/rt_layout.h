@@ -134,7 +134,7 @@ constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep 
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
-constexpr uint32_t kWaveTraceWords = 13;
+constexpr uint32_t kWaveTraceWords = 21;   // rt_body.h: timeline, phases, tail-round phases
 
 // Resident 256-thread blocks per CU allowed by the VGPR budget: 512 VGPRs per lane per SIMD, one
 // wave of each block per SIMD.  The persistent grid must never exceed residency (a block that starts
@@ -191,6 +191,7 @@ struct RenderArgs {
   uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of
                                   // the longest-first order) run their wave at raised issue priority
   uint32_t prio_chunk;            // < 64: those ids are handed out in pieces of this many (work[1])
+  uint32_t prio_lanes;            // < 64: a wave holds at most this many of them and nothing else meanwhile
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the
                                   // wave still need a try (they resume next round; 0 = never early)
   uint32_t black_skip;            // every attenuation is finite (host-checked): a path ending in

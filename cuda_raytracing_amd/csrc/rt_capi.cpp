@@ -143,7 +143,9 @@ struct rt_context {
   rt::SphereAccel accel;
   bool accel_ok = false;
   uint32_t accel_nodes = 0, accel_prims = 0;   // word offsets in the device image
-  uint32_t accel_lds_nodes = 0;                 // top SAH nodes staged in LDS (RT_ACCEL_LDS_NODES)
+  // top SAH nodes staged in LDS (RT_ACCEL_LDS_NODES): 64 (6 levels, 4 KiB per block) measured best on
+  // the 10k scene, 1-3 % over none and over 128 / 256 (profiles/r03_ab_accel_lds_bfs_early*.jsonl)
+  uint32_t accel_lds_nodes = 64;
   // verified mixed-world traversal (RT_TRAV_MIXED): macro roots marked in the image, SAH words appended
   rt::MixedAccel mixed;
   bool mixed_ok = false;
@@ -172,6 +174,7 @@ struct rt_context {
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
   int prio_chunk = -1;                          // RT_PRIO_CHUNK: those tiles handed out in pieces of this many pixels
+  int prio_lanes = 0;                           // RT_PRIO_LANES: waves holding them keep at most this many lanes busy
                                                 // (-1 auto: 1 with cooperative noise, else whole tiles)
   uint32_t coop_noise = 32;                     // RT_COOP_NOISE: cooperative noise octaves when <= this many lanes
                                                 // of a wave need one (0 = never, max 32)
@@ -298,6 +301,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
+  if (const char *e = std::getenv("RT_PRIO_LANES")) c->prio_lanes = std::atoi(e);
   if (const char *e = std::getenv("RT_COOP_NOISE")) c->coop_noise = static_cast<uint32_t>(std::min(32, std::max(0, std::atoi(e))));
   if (const char *e = std::getenv("RT_PRIO_CHUNK")) {
     const int v = std::atoi(e);
@@ -653,6 +657,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.defer_trace = c->defer_trace;
   a.trace_min_iters = c->trace_min_iters;
   a.prio_chunk = 64u;   // whole tiles unless the longest-first schedule splits its costliest ones
+  a.prio_lanes = 64u;   // no sparse waves (the probe launch keeps these defaults)
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;
@@ -706,6 +711,11 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     // single pixels; scene 0 and Cornell lose 4-10 % with split tiles, so they keep whole tiles)
     const int pcn = c->prio_chunk >= 0 ? c->prio_chunk : ((c->img.has_noise && c->coop_noise) ? 1 : 64);
     a.prio_chunk = a.prio_ids ? static_cast<uint32_t>(pcn) : 64u;
+    // RT_PRIO_LANES (A/B): waves holding those pixels stay sparse (single-pixel hand-out)
+    if (a.prio_ids && c->prio_lanes > 0 && c->prio_lanes < 64) {
+      a.prio_lanes = static_cast<uint32_t>(c->prio_lanes);
+      a.prio_chunk = 1u;
+    }
   }
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)

@@ -19,4 +19,7 @@ run c3_scene1_cornell ${LIM:-300} --scene 1 --spp 1024 --bounces 50 --steps 3 --
 run c3_scene17_perlin ${LIM:-300} --scene 17 --spp 1024 --bounces 50 --steps 3 --warmup 1
 run c4_scene20_10k ${LIM:-300} --scene 20 --spp 256 --bounces 16 --steps 3 --warmup 1
 run c5_scene0_4k ${LIM:-300} --scene 0 --width 3840 --height 2160 --spp 2048 --bounces 50 --steps 2 --warmup 1
+# final_scene (raytracing.cu:2151-2202; §8f row 1, not a BASELINE config) at the reference's 800x800, d40,
+# a bounded spp (the reference's own spp would take minutes per frame)
+[ -n "${WITH_FINAL:-}" ] && run c6_scene3_final ${LIM:-300} --scene 3 --width 800 --height 800 --spp 64 --bounces 40 --steps 2 --warmup 1
 cat gpurun_out/configs.jsonl

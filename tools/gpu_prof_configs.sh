@@ -17,3 +17,4 @@ run c3_scene1_cornell --scene 1 --spp 1024 --bounces 50
 run c3_scene17_perlin --scene 17 --spp 1024 --bounces 50
 run c4_scene20_10k --scene 20 --spp 256 --bounces 16
 run c5_scene0_4k --scene 0 --width 3840 --height 2160 --spp 2048 --bounces 50
+run c6_scene3_final --scene 3 --width 800 --height 800 --spp 64 --bounces 40

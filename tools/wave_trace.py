@@ -27,7 +27,7 @@ import cuda_raytracing_amd as rt  # noqa: E402
 w, s = rt.build_scene(a.scene)
 cam, W, H = rt.camera_from_settings(s, a.width, a.height)
 fb, st = rt.render(w.scene(), cam, rt.make_params(s, W, H, spp=a.spp, bounces=a.bounces), with_stats=True)
-rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 13)
+rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 21)
 rec = rec[rec[:, 1] > 0]
 t0 = rec[:, 0].min()
 start = (rec[:, 0] - t0).astype(np.float64)
@@ -57,6 +57,18 @@ for w in top:
           f"tiles {int(r[2])} us/round {(end[w] - start[w]) / 100 / max(int(r[4]), 1):.2f} phases (cycles/round): "
           + " ".join(f"{n} {v / max(int(r[4]), 1):.0f}" for n, v in
                      zip(("refill", "trace", "back", "mat", "rej", "unwind", "cam"), ph)))
+# the rounds with at most 2 busy lanes (the tail: trapped pixels alone in their wave)
+lr = rec[:, 13].astype(np.float64)
+lph = rec[:, 14:21].astype(np.float64)
+if lr.sum() > 0:
+    tot = lph.sum(axis=0)
+    print("tail rounds (<= 2 busy lanes): %d total, %.1f%% of all rounds; cycles/round: " % (lr.sum(), 100 * lr.sum() / rounds.sum())
+          + " ".join(f"{n} {v / lr.sum():.0f}" for n, v in zip(("refill", "trace", "back", "mat", "rej", "unwind", "cam"), tot)))
+    for w in top[:3]:
+        if rec[w, 13] > 0:
+            print(f"  straggler wave {w}: tail rounds {int(rec[w, 13])} cycles/round: "
+                  + " ".join(f"{n} {v / rec[w, 13]:.0f}" for n, v in
+                             zip(("refill", "trace", "back", "mat", "rej", "unwind", "cam"), rec[w, 14:21].astype(np.float64))))
 # per dispatch rank: block b reaches its CU in round b // n_cu of the dispatch (n_cu = 256 blocks
 # per round on MI355X), so its waves are the (b // n_cu)-th oldest of their SIMDs
 wid = np.arange(len(rec))
