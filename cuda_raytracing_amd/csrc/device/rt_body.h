@@ -1569,6 +1569,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool probe_end = false;                  // probe: the lane's path ended in the last round
   uint64_t ph_refill = 0, ph_trace = 0, ph_rej = 0, ph_mat = 0, ph_shade = 0, ph_unwind = 0, ph_cam = 0, t_mark = 0;   // wave-trace clocks
   uint64_t busy_lane_rounds = 0;
+  uint64_t ph_noise = 0, lph_noise = 0;                     // wave trace: cooperative noise (part of mat)
   uint64_t lph[7] = {0, 0, 0, 0, 0, 0, 0}, lone_rounds = 0;   // wave trace: the same phases over the rounds
   bool lone = false;                                         // with at most 2 busy lanes (the frame's tail)
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1803,6 +1804,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     // wave needs one, the octaves are spread over 2, 4 or 8 lanes per noise lane (coop_noise_code) ----
     bool coop = false;
     uint32_t coop_code = 0;
+    const uint64_t t_noise0 = TRACE ? __builtin_amdgcn_s_memtime() : 0;
     if (COOP && !COUNT && (TM & (1u << T_NOISE))) {
       bool nz = false;
       uint32_t ntb = 0;
@@ -1823,6 +1825,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         else coop_code = coop_noise_code<2>(S, A, nm, lane, lt_mask, h.p, ntb, nsc);
         coop = nz;
       }
+    }
+    if (TRACE) {   // the cooperative noise block's share of the material phase
+      const uint64_t dt = __builtin_amdgcn_s_memtime() - t_noise0;
+      ph_noise += dt;
+      if (lone) lph_noise += dt;
     }
     if (busy && T.result && !pending) {
       const uint32_t mbase = A.off_mats + h.mat * kMatWords;
@@ -1990,6 +1997,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     w[12] = ph_cam;
     w[13] = lone_rounds;
     for (int k = 0; k < 7; ++k) w[14 + k] = lph[k];
+    w[21] = ph_noise; w[22] = lph_noise;
   }
   if (COUNT) {
     uint32_t vals[CNT_SLOTS] = {0};

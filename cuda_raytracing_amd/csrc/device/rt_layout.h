@@ -134,7 +134,7 @@ constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep 
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
-constexpr uint32_t kWaveTraceWords = 21;   // rt_body.h: timeline, phases, tail-round phases
+constexpr uint32_t kWaveTraceWords = 23;   // rt_body.h: timeline, phases, tail-round phases, noise share
 
 // Resident 256-thread blocks per CU allowed by the VGPR budget: 512 VGPRs per lane per SIMD, one
 // wave of each block per SIMD.  The persistent grid must never exceed residency (a block that starts

@@ -72,6 +72,8 @@ constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
+constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
+constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
 constexpr uint32_t kRcLdsMaxLevels = 256;  // colour-stack levels kept in LDS at most (max_bounces is a u8)
 
 // LDS bytes of one colour-stack level for a 256-thread block: 32-bit codes, or 16-bit in narrow kernels
@@ -175,6 +177,7 @@ struct rt_context {
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
   int prio_chunk = -1;                          // RT_PRIO_CHUNK: those tiles handed out in pieces of this many pixels
   int prio_lanes = 0;                           // RT_PRIO_LANES: waves holding them keep at most this many lanes busy
+                                                // (0: the default, kSparseLanes on noise scenes; 64: off)
                                                 // (-1 auto: 1 with cooperative noise, else whole tiles)
   uint32_t coop_noise = 32;                     // RT_COOP_NOISE: cooperative noise octaves when <= this many lanes
                                                 // of a wave need one (0 = never, max 32)
@@ -702,18 +705,25 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), s) != hipSuccess)
       return RT_ERR_HIP;
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
-    const int pt = c->prio_tiles >= 0 ? c->prio_tiles : kPrioTiles;
+    // noise scenes: sparse hot waves (below) by default, over the 16 costliest tiles
+    const bool noise_sched = c->img.has_noise && c->coop_noise;
+    const int lanes_hot = c->prio_lanes != 0 ? c->prio_lanes : (noise_sched ? kSparseLanes : 0);
+    const int pt = c->prio_tiles >= 0 ? c->prio_tiles : ((lanes_hot > 0 && lanes_hot < 64) ? kSparseTiles : kPrioTiles);
     a.prio_ids = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(pt) * 64u, a.n_ids));
     // The costliest tiles of a noise scene hold pixels whose paths are trapped between noise surfaces
     // (the Perlin scene's contact point: ~35k serial rounds per pixel); handed out one pixel at a time
     // they spread over many waves, each with few noise lanes, whose octaves the idle lanes then share
     // (measured on scene 17, d50, spp 1024: 204 ms whole tiles without cooperation, 168 with, 135 with
     // single pixels; scene 0 and Cornell lose 4-10 % with split tiles, so they keep whole tiles)
-    const int pcn = c->prio_chunk >= 0 ? c->prio_chunk : ((c->img.has_noise && c->coop_noise) ? 1 : 64);
+    const int pcn = c->prio_chunk >= 0 ? c->prio_chunk : (noise_sched ? 1 : 64);
     a.prio_chunk = a.prio_ids ? static_cast<uint32_t>(pcn) : 64u;
-    // RT_PRIO_LANES (A/B): waves holding those pixels stay sparse (single-pixel hand-out)
-    if (a.prio_ids && c->prio_lanes > 0 && c->prio_lanes < 64) {
-      a.prio_lanes = static_cast<uint32_t>(c->prio_lanes);
+    // Sparse hot waves: a wave holding pixels of those tiles keeps at most lanes_hot of them busy and takes
+    // no other pixel meanwhile, so the trapped chains run in waves with few divergent lanes (and issue
+    // priority) for the whole frame, not only once the rest is done (single-pixel hand-out).  Scene 17:
+    // 135-139 -> 99-101 ms per frame, scene 19: 205 -> 165; scene 0 +12 %, Cornell +5 %, 10k +-3 %, so
+    // noise scenes only (profiles/r03_ab_sparse_hot_waves_*.jsonl).  RT_PRIO_LANES=64 turns it off.
+    if (a.prio_ids && lanes_hot > 0 && lanes_hot < 64) {
+      a.prio_lanes = static_cast<uint32_t>(lanes_hot);
       a.prio_chunk = 1u;
     }
   }

@@ -660,12 +660,14 @@ def test_code_object_disk_cache(tmp_path):
 
 @pytest.mark.parametrize("idx", [17, 19])
 @pytest.mark.parametrize("env", [{}, {"RT_COOP_NOISE": "0"}, {"RT_COOP_NOISE": "8", "RT_PRIO_CHUNK": "64"},
-                                 {"RT_PRIO_CHUNK": "8"}, {"RT_PRIO_LANES": "2", "RT_PRIO_TILES": "6"},
+                                 {"RT_PRIO_LANES": "64", "RT_PRIO_CHUNK": "8"}, {"RT_PRIO_LANES": "64"},
+                                 {"RT_PRIO_LANES": "2", "RT_PRIO_TILES": "6"},
                                  {"RT_PRIO_LANES": "1", "RT_PRIO_TILES": "300"}])
 def test_cooperative_noise_octaves_vs_oracle(idx, env, monkeypatch):
     # noise scenes: perlin_turbulence's octaves spread over 2/4/8 lanes per noise lane (render_body's
     # cooperative block), the costliest tiles handed out pixel by pixel, waves holding them kept sparse
-    # (RT_PRIO_LANES; 300 tiles = every tile of this frame) — the frame is the oracle's
+    # (the default on noise scenes; RT_PRIO_LANES=64 turns it off; 300 tiles = every tile of this
+    # frame) — the frame is the oracle's
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     w, s = rt.build_scene(idx)

@@ -27,7 +27,7 @@ import cuda_raytracing_amd as rt  # noqa: E402
 w, s = rt.build_scene(a.scene)
 cam, W, H = rt.camera_from_settings(s, a.width, a.height)
 fb, st = rt.render(w.scene(), cam, rt.make_params(s, W, H, spp=a.spp, bounces=a.bounces), with_stats=True)
-rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 21)
+rec = np.fromfile(path, dtype=np.uint64).reshape(-1, 23)
 rec = rec[rec[:, 1] > 0]
 t0 = rec[:, 0].min()
 start = (rec[:, 0] - t0).astype(np.float64)
@@ -64,6 +64,8 @@ if lr.sum() > 0:
     tot = lph.sum(axis=0)
     print("tail rounds (<= 2 busy lanes): %d total, %.1f%% of all rounds; cycles/round: " % (lr.sum(), 100 * lr.sum() / rounds.sum())
           + " ".join(f"{n} {v / lr.sum():.0f}" for n, v in zip(("refill", "trace", "back", "mat", "rej", "unwind", "cam"), tot)))
+    print("  of which cooperative noise (in mat): all rounds %.0f cycles/round, tail rounds %.0f"
+          % (rec[:, 21].astype(np.float64).sum() / rounds.sum(), rec[:, 22].astype(np.float64).sum() / lr.sum()))
     for w in top[:3]:
         if rec[w, 13] > 0:
             print(f"  straggler wave {w}: tail rounds {int(rec[w, 13])} cycles/round: "
