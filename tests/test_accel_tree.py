@@ -92,6 +92,18 @@ def test_tree_covers_every_sphere_once(idx):
 
 
 @pytest.mark.parametrize("idx", [2, rt.RT_SCENE_RANDOM_10K])
+def test_nodes_are_breadth_first(idx):
+    # accel_build.h bfs_order: the root is node 0 and the internal children, listed node by node, are
+    # nodes 1, 2, 3, ...: every prefix of the array is a complete top of the tree (the LDS-staged part)
+    w, _ = rt.build_scene(idx)
+    info, nodes, _ = rt.accel_build(w.scene())
+    nodes = nodes.reshape(-1, 16)
+    assert info["root"] == 0
+    kids = [int(nodes[i, 12 + c]) for i in range(len(nodes)) for c in range(2) if not (int(nodes[i, 12 + c]) & LEAF)]
+    assert kids == list(range(1, len(nodes)))
+
+
+@pytest.mark.parametrize("idx", [2, rt.RT_SCENE_RANDOM_10K])
 def test_verification_boxes_are_reference_ancestors(idx):
     w, _ = rt.build_scene(idx)
     sc = w.scene()
