@@ -891,7 +891,7 @@ struct AccelTraceK {
     bool nice = (ao <= 1.0e6f) && (dmin >= 1.0e-20f) && (dmax <= 1.0e6f) && (dmax >= 7.0e-7f);
     const Trav tsave = T;
     const Hit hsave = h;
-    bool tie = resume && T.atie != 0;
+    bool tie = resume && (T.anode >> 31) != 0;
     uint32_t best = resume ? T.abest : 0u;
     const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
     const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.accel_prims);
@@ -903,8 +903,8 @@ struct AccelTraceK {
       const SlabRay sr = slab_ray(T, oinv, pinv);
       const float sa2 = 2.0f * dot(r.d, r.d);   // sphere_hit_tie's per-ray terms
       const float sra2 = rcp_ref(sa2);
-      uint32_t node = resume ? T.anode : A.accel_root;
-      int sp = resume ? T.asp : 0;
+      uint32_t node = resume ? (T.anode & 0xffffu) : A.accel_root;
+      int sp = resume ? static_cast<int>((T.anode >> 16) & 0x7fffu) : 0;
       // Wave-uniform loop, one node per walking lane per step.  Rays differ wildly in length (the
       // horizon of a sphere field vs a close hit), so instead of every lane waiting for the longest
       // walk, the round's walk ends once few lanes remain (A.defer_trace, after A.trace_min_iters
@@ -966,7 +966,8 @@ struct AccelTraceK {
         if (!COUNT && it >= A.trace_min_iters && nl <= A.defer_trace && 4 * nl <= started) break;
       }
       if (walking) {   // paused: resume next round
-        T.active = 1; T.anode = node; T.asp = sp; T.abest = best; T.atie = tie ? 1u : 0u;
+        // one VGPR for node (< 2^16, u16 stack entries), depth and the tie flag
+        T.active = 1; T.anode = node | (static_cast<uint32_t>(sp) << 16) | (tie ? 0x80000000u : 0u); T.abest = best;
         return;
       }
     }
