@@ -1080,7 +1080,10 @@ __device__ __forceinline__ float sphere_value(const Ray &r, f3 c0, f3 mv, float 
   return root;
 }
 
-template <uint32_t KM>
+// PAUSE: as in LaneTraceK, the round's walk may stop once few lanes still walk; it stops only between two
+// reference steps (no lane inside a macro walk), where the whole walk state is T, the ray (drift included),
+// the hit record and the LDS stack, all of which outlive the round.
+template <uint32_t KM, bool PAUSE = false>
 struct MixedTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t lanes,
@@ -1090,9 +1093,11 @@ struct MixedTraceK {
       return;
     }
     if (!busy) return;
-    trav_reset(T, r);
-    stk[0] = static_cast<uint16_t>(A.root);
-    T.sp = 1;
+    if (!PAUSE || !T.active) {
+      trav_reset(T, r);
+      stk[0] = static_cast<uint16_t>(A.root);
+      T.sp = 1;
+    }
     T.active = 0;
     const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.mix_nodes);
     const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.mix_prims);
@@ -1103,7 +1108,40 @@ struct MixedTraceK {
     bool tie = false;
     SlabRay sr;
     sr.on = mk(0, 0, 0); sr.of = mk(0, 0, 0); sr.nx = sr.ny = sr.nz = false;
-    while (__ballot(walking) != 0) {
+#ifdef RT_MIX_DIAG
+    // diagnostic build (RT_JIT_OPTS=-DRT_MIX_DIAG): wave trips, lanes per phase, reference steps by kind;
+    // every value is wave-uniform (ballots at the top of a trip, where all the wave's walkers are active)
+    unsigned long long dg[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    dg[9] = __popcll(__ballot(true));
+#endif
+    const uint32_t started = PAUSE ? static_cast<uint32_t>(__popcll(__ballot(true))) : 0u;
+    uint32_t it = 0;
+    for (;;) {
+      const uint64_t wl = __ballot(walking);
+      if (wl == 0) break;
+      if (PAUSE) {
+        const uint32_t nl = static_cast<uint32_t>(__popcll(wl));
+        if (++it >= A.trace_min_iters && nl <= A.defer_trace && 4 * nl <= started && __ballot(in_macro) == 0) {
+          T.active = walking && T.sp > 0 ? 1u : 0u;   // resumes next round with shading skipped
+          break;
+        }
+      }
+#ifdef RT_MIX_DIAG
+      {
+        const bool rs = walking && !in_macro && T.sp != 0;
+        const uint64_t rl = __ballot(rs), ml = __ballot(walking && in_macro);
+        const uint32_t k = rs ? S.w4(stk[(T.sp - 1) * 64] * kNodeWords).x : 0xffu;
+        const uint64_t bv = __ballot(k == K_BVH), qd = __ballot(k == K_QUAD || k == K_TRIANGLE),
+                       ch = __ballot(k == K_TRANSLATE || k == K_YROTATE);
+        dg[0]++;
+        dg[1] += __popcll(rl);
+        dg[2] += __popcll(ml);
+        dg[3] += (rl != 0 && ml != 0) ? 1u : 0u;
+        dg[4] += (rl != 0) ? 1u : 0u;
+        dg[5] += __popcll(bv); dg[6] += __popcll(qd); dg[7] += __popcll(ch);
+        dg[8] += (bv != 0) + (qd != 0) + (ch != 0) + ((rl & ~(bv | qd | ch)) != 0);
+      }
+#endif
       if (!walking) continue;
       if (!in_macro) {
         if (T.sp == 0) { walking = false; continue; }
@@ -1135,13 +1173,24 @@ struct MixedTraceK {
             const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
             const bool rot = !tr || (chain & kChainRotate);
             float sn = asf(w0.z), cs = asf(w0.w);
-            if (tr) {
-              translate_enter(T, r, off);
-              if (rot) { const uint4 c0 = S.w4(w0.y * kNodeWords); sn = asf(c0.z); cs = asf(c0.w); }
+            uint4 g0, g1, g2, g3, g4;
+            if (chain & kChainPacked) {
+              // a sphere chain packed into its head record (mixed_accel.cpp): no dependent loads
+              if (rot) { sn = asf(w3.y); cs = asf(w3.z); }
+              g0 = make_uint4(K_SPHERE, w1.y, w1.z, w1.w);
+              g1 = w4;
+              g2 = w2;
+              g3 = g2; g4 = g2;
+              if (tr) translate_enter(T, r, off);
+            } else {
+              if (tr) {
+                translate_enter(T, r, off);
+                if (rot) { const uint4 c0 = S.w4(w0.y * kNodeWords); sn = asf(c0.z); cs = asf(c0.w); }
+              }
+              const uint32_t gb = (chain & kChainPrimMask) * kNodeWords;
+              g0 = S.w4(gb); g1 = S.w4(gb + 4); g2 = S.w4(gb + 8); g3 = S.w4(gb + 12); g4 = S.w4(gb + 16);
             }
             if (rot) rotate_enter(T, r, sn, cs);
-            const uint32_t gb = (chain & kChainPrimMask) * kNodeWords;
-            const uint4 g0 = S.w4(gb), g1 = S.w4(gb + 4), g2 = S.w4(gb + 8), g3 = S.w4(gb + 12), g4 = S.w4(gb + 16);
             if ((KM & (1u << K_SPHERE)) && g0.x == K_SPHERE)
               sphere_hit<UV>(T, r, h, g0.y, mk(asf(g0.z), asf(g0.w), asf(g1.x)), mk(asf(g1.y), asf(g1.z), asf(g1.w)),
                              asf(g2.y), asf(g2.z), true);
@@ -1317,6 +1366,12 @@ struct MixedTraceK {
         T.sp = sp;
       }
     }
+#ifdef RT_MIX_DIAG
+    if (A.mix_fallbacks && __builtin_amdgcn_readfirstlane(lane) == lane) {
+      unsigned long long *d = reinterpret_cast<unsigned long long *>(A.mix_fallbacks + 5);
+      for (int i = 0; i < 10; ++i) atomicAdd(d + i, dg[i]);
+    }
+#endif
   }
 };
 

@@ -53,7 +53,13 @@ constexpr uint32_t kMacroStatic = 0x80000000u, kMacroDynamic = 0x40000000u, kMac
 // Transform chains (translate -> [y-rotate ->] primitive, or y-rotate -> primitive): W_MACRO of the head
 // record = kChainFused [| kChainRotate: the translate's child is a y-rotation] | the primitive's record.
 // MixedTraceK runs the reference's five stack steps of such a chain (:1176-1237) as one.
-constexpr uint32_t kChainFused = 0x20000000u, kChainRotate = 0x10000000u, kChainPrimMask = 0x0000ffffu;
+// kChainPacked: the chain ends in a sphere whose record words sit in the head's unused words, so the fused
+// step needs no further load: sphere words 1..3 (material, centre x, y) at head words 5..7, sphere words
+// 4..7 (centre z, motion) at 16..19, sphere words 8..11 (radius, radius^2, 1/radius) at 8..11, the
+// y-rotation's sin / cos at 13 / 14.
+constexpr uint32_t kChainFused = 0x20000000u, kChainRotate = 0x10000000u, kChainPacked = 0x08000000u,
+                   kChainPrimMask = 0x0000ffffu;
+enum : int { W_PK_SPHERE0 = 5, W_PK_SPHERE8 = 8, W_PK_SIN = 13, W_PK_COS = 14, W_PK_SPHERE4 = 16 };
 constexpr int kMixPrimWords = 32;
 enum : int { MP_GROUP = 20, MP_GBOX = 21, MP_RECORD = 27 };
 constexpr uint32_t kMixNoGroup = 0xffffffffu;
@@ -141,8 +147,9 @@ constexpr uint32_t kWaveTraceWords = 23;   // rt_body.h: timeline, phases, tail-
 // late only lengthens the tail).  Measured on gfx950 with per-wave start stamps (tools/wave_trace.py):
 // kernels of 70 and 75 VGPRs ran 6 resident blocks/CU although the occupancy API reported 7, and
 // 80-86 VGPRs ran 5: consistent with an allocation granule of 16 for wave64, which is used here.
-inline int resident_blocks_by_vgprs(int vgprs) {
-  const int alloc = ((vgprs > 0 ? vgprs : 1) + 15) / 16 * 16;
+inline int resident_blocks_by_vgprs(int vgprs, int granule = 16) {
+  const int g = granule == 8 ? 8 : 16;
+  const int alloc = ((vgprs > 0 ? vgprs : 1) + g - 1) / g * g;
   const int w = 512 / alloc;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }

@@ -39,7 +39,7 @@ bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel
 // primitives.  build_mixed_accel also writes W_MACRO / W_XFBOX into `img`'s node words.
 struct MixedAccel {
   std::vector<uint32_t> node_words, prim_words;
-  uint32_t macros = 0, dynamic = 0, prims = 0, depth = 0;
+  uint32_t macros = 0, dynamic = 0, prims = 0, depth = 0, packed = 0;   // packed: sphere chains (kChainPacked)
 };
 // false (with a reason) when no node qualifies (e.g. a world of transforms only)
 bool build_mixed_accel(SceneImage *img, MixedAccel *out, std::string *why);

@@ -251,19 +251,37 @@ bool build_mixed_accel(SceneImage *img, MixedAccel *out, std::string *why) {
   }
   if (out->macros == 0) { if (why) *why = "no transform-free subtree"; return false; }
   if (bd.nodes.size() / kAccelNodeWords >= 65536) { if (why) *why = "SAH trees too large for u16 stack entries"; return false; }
-  // transform chains ending in a primitive: one fused step in the kernel (W_MACRO of the chain's head)
+  // transform chains ending in a primitive: one fused step in the kernel (W_MACRO of the chain's head); a
+  // chain ending in a sphere also carries the sphere's words (and the rotation's sin / cos) in the head's
+  // unused words 5..11 and 13..19 (kChainPacked, rt_layout.h).  RT_MIX_PACK=0 (A/B) keeps the loads.
+  const char *pk_env = std::getenv("RT_MIX_PACK");
+  const bool pack = !(pk_env && pk_env[0] == '0');
   for (uint32_t r = 0; r < img->node_count; ++r) {
     uint32_t *w = &img->words[static_cast<size_t>(r) * kNodeWords];
-    if (w[W_KIND] != K_TRANSLATE && w[W_KIND] != K_YROTATE) continue;   // words 12..19 unused by both
+    if (w[W_KIND] != K_TRANSLATE && w[W_KIND] != K_YROTATE) continue;   // words 5..19 unused by both
     const uint32_t c = w[W_AUX];
     if (c >= img->node_count) continue;
     const uint32_t ck = an.node(c)[W_KIND];
+    uint32_t prim = ~0u, rot = ~0u;
     if (Analysis::is_prim(ck)) {
-      w[W_MACRO] = kChainFused | c;
+      prim = c;
+      if (w[W_KIND] == K_YROTATE) rot = r;
     } else if (w[W_KIND] == K_TRANSLATE && ck == K_YROTATE) {
       const uint32_t g = an.node(c)[W_AUX];
-      if (g < img->node_count && Analysis::is_prim(an.node(g)[W_KIND])) w[W_MACRO] = kChainFused | kChainRotate | g;
+      if (g < img->node_count && Analysis::is_prim(an.node(g)[W_KIND])) { prim = g; rot = c; }
     }
+    if (prim == ~0u || prim > kChainPrimMask) continue;
+    uint32_t mw = kChainFused | (w[W_KIND] == K_TRANSLATE && rot != ~0u ? kChainRotate : 0u) | prim;
+    const uint32_t *pw = an.node(prim);
+    if (pack && pw[W_KIND] == K_SPHERE) {
+      for (int j = 0; j < 3; ++j) w[W_PK_SPHERE0 + j] = pw[1 + j];
+      for (int j = 0; j < 4; ++j) w[W_PK_SPHERE4 + j] = pw[4 + j];
+      for (int j = 0; j < 4; ++j) w[W_PK_SPHERE8 + j] = pw[8 + j];
+      if (rot != ~0u) { w[W_PK_SIN] = an.node(rot)[W_SIN]; w[W_PK_COS] = an.node(rot)[W_COS]; }
+      mw |= kChainPacked;
+      out->packed++;
+    }
+    w[W_MACRO] = mw;
   }
   for (uint32_t r = 0; r < img->node_count; ++r) {
     uint32_t *w = &img->words[static_cast<size_t>(r) * kNodeWords];

@@ -357,7 +357,8 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
             hipMemcpy(c->scene.p, dev_words.data(), dev_words.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
             c->jump.ensure(J.size() * 4) == hipSuccess &&
             hipMemcpy(c->jump.p, J.data(), J.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
-            c->work.ensure(64) == hipSuccess &&
+            c->work.ensure(256) == hipSuccess &&   // 16 words + the mixed-walk diagnostic (RT_MIX_DIAG)
+           
             c->counters.ensure(RT_CNT__COUNT * sizeof(unsigned long long)) == hipSuccess;
   for (hipEvent_t &e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
   if (!ok) { rt_context_destroy(c); return RT_ERR_HIP; }
@@ -672,7 +673,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     a.wave_trace = static_cast<unsigned long long *>(c->wave_trace.p);
   }
 
-  if (hipMemsetAsync(c->work.p, 0, 64, s) != hipSuccess) return RT_ERR_HIP;
+  if (hipMemsetAsync(c->work.p, 0, 256, s) != hipSuccess) return RT_ERR_HIP;
   if (c->counted && hipMemsetAsync(c->counters.p, 0, RT_CNT__COUNT * 8, s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[0], s) != hipSuccess) return RT_ERR_HIP;
   if (rt::launch_seed(sa, s) != hipSuccess) return RT_ERR_HIP;
@@ -786,6 +787,13 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
     st->mix_fallbacks = w[11];
     if (std::getenv("RT_DEBUG"))
       std::fprintf(stderr, "[rt] mixed walk fallbacks: %u (tie %u, reach %u; probe %u)\n", w[11], w[2], w[3], w[10]);
+    unsigned long long dg[10];
+    if (hipMemcpy(dg, static_cast<uint32_t *>(c->work.p) + 16, sizeof dg, hipMemcpyDeviceToHost) != hipSuccess)
+      return RT_ERR_HIP;
+    if (dg[0] && std::getenv("RT_DEBUG"))   // RT_JIT_OPTS=-DRT_MIX_DIAG builds only
+      std::fprintf(stderr, "[rt] mixed diag: trips %llu ref_lanes %llu macro_lanes %llu both %llu ref_trips %llu "
+                   "bvh %llu planar %llu chain %llu kind_groups %llu walk_lanes %llu\n", dg[0], dg[1], dg[2], dg[3],
+                   dg[4], dg[5], dg[6], dg[7], dg[8], dg[9]);
   }
   st->init_ms = a;
   st->sched_ms = b;

@@ -345,7 +345,10 @@ std::string jit_accel_source(const SceneImage &img, int variant) {
 
 std::string jit_mixed_source(const SceneImage &img, int variant) {
   const int v = variant & kJitVarMask;
-  const std::string mt = "MixedTraceK<" + std::to_string(scene_kinds(img)) + "u>";
+  // pausable walk (RT_MIX_PAUSE=0: the round waits for every walk, A/B)
+  const char *pe = std::getenv("RT_MIX_PAUSE");
+  const bool pause = !(pe && pe[0] == '0');
+  const std::string mt = "MixedTraceK<" + std::to_string(scene_kinds(img)) + "u, " + (pause ? "true" : "false") + ">";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr() + " void rt_mixed_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarNoProbe) + ", " + mt + ">(A);\n}\n";
@@ -387,7 +390,8 @@ int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes) {
   int vgprs = 0;
   const hipError_t e = hipFuncGetAttribute(&vgprs, HIP_FUNC_ATTRIBUTE_NUM_REGS, fn);
   const int api = n;
-  if (e == hipSuccess) n = std::min(n, resident_blocks_by_vgprs(vgprs));
+  const char *ge = std::getenv("RT_VGPR_GRANULE");   // A/B: 8 = the occupancy table's granule
+  if (e == hipSuccess) n = std::min(n, resident_blocks_by_vgprs(vgprs, ge ? std::atoi(ge) : 16));
   if (std::getenv("RT_DEBUG"))
     std::fprintf(stderr, "[rt] jit occupancy: api %d blocks/CU, NUM_REGS %d (%s) -> %d, lds %zu B\n", api, vgprs,
                  hipGetErrorString(e), n, lds_bytes);

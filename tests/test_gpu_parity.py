@@ -827,6 +827,23 @@ def test_mixed_walk_fallback_path_vs_oracle(monkeypatch):
     assert np.array_equal(bits(fb), bits(ref))
 
 
+@pytest.mark.parametrize("env", [{"RT_DEFER_TRACE": "64", "RT_TRACE_MIN": "1"}, {"RT_MIX_PAUSE": "0"},
+                                 {"RT_MIX_PACK": "0"}, {"RT_MIX_PAUSE": "0", "RT_MIX_PACK": "0"}])
+def test_mixed_walk_pause_and_packed_chains(monkeypatch, env):
+    # the walk paused between reference steps (forced early: any round with <= 1/4 of its walkers left)
+    # and sphere chains packed into their head records, each on and off, vs the oracle
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for w, s, size, spp, b in ((*rt.build_scene(3), 72, 3, 40), (*_mixed_world(2), 64, 4, 12)):
+        cam, W, H = rt.camera_from_settings(s, size, size)
+        p = rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_MIXED)
+        rc, ref, _ = oracle_render(w.scene(), cam, p)
+        assert rc == 0
+        fb, st = gpu(w.scene(), cam, p)
+        assert st.traversal == rt.RT_TRAV_MIXED
+        assert np.array_equal(bits(fb), bits(ref)), env
+
+
 def test_mixed_walk_final_scene_full_size_rows():
     # the final_scene frame (800x800, d40) at reduced spp: every 61st row (first and last) vs the oracle
     w, s = rt.build_scene(3)

@@ -36,7 +36,7 @@ for cfg in (args or [""]):
         k, v = kv.split("=", 1)
         env[k] = v
     r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=600)
-    occ = [l for l in r.stderr.splitlines() if "launch:" in l or "occupancy" in l or "fallbacks" in l][-3:]
+    occ = [l for l in r.stderr.splitlines() if "launch:" in l or "occupancy" in l or "fallbacks" in l or "diag" in l][-4:]
     print(json.dumps({"cfg": cfg, "result": r.stdout.strip().splitlines()[-1] if r.stdout.strip() else r.stderr[-800:],
                       "debug": occ}), flush=True)
     if r.returncode != 0:
