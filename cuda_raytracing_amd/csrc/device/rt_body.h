@@ -540,7 +540,7 @@ __device__ __forceinline__ void planar_hit(Trav &T, const Ray &r, Hit &h, bool t
 // sphere branch (:1093-1123) + sphere_get_uv (:583-590, image textures only)
 template <bool UV>
 __device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
-                                           float inv_rad, bool in_xf) {
+                                           float inv_rad, bool in_xf, bool need_uv = true) {
   f3 center = line_at(c0, r.time, mv);
   f3 oc = sub(center, r.o);
   float a = dot(r.d, r.d);
@@ -556,7 +556,7 @@ __device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32
       h.p = line_at(r.o, root, r.d);
       h.mat = mat;
       f3 outward = scale(inv_rad, sub(h.p, center));
-      if (UV) {
+      if (UV && need_uv) {
         const float pi = 3.1415926535897932385f;
         float theta = rt_acosf(-outward.y);
         float phi = rt_atan2f(-outward.z, outward.x) + pi;
@@ -812,13 +812,14 @@ __device__ __forceinline__ bool accel_box(const Trav &T, const SlabRay &R, float
 // after the last step (sphere_commit, from the closest sphere's index) instead of at every acceptance:
 // the same operations on the same values, outside the loop.
 template <bool UV>
-__device__ __forceinline__ void sphere_commit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float inv_rad) {
+__device__ __forceinline__ void sphere_commit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float inv_rad,
+                                              bool need_uv = true) {
   const f3 center = line_at(c0, r.time, mv);
   h.t = T.tmax;
   h.p = line_at(r.o, h.t, r.d);
   h.mat = mat;
   f3 outward = scale(inv_rad, sub(h.p, center));
-  if (UV) {
+  if (UV && need_uv) {
     const float pi = 3.1415926535897932385f;
     float theta = rt_acosf(-outward.y);
     float phi = rt_atan2f(-outward.z, outward.x) + pi;
@@ -1163,7 +1164,7 @@ struct MixedTraceK {
                      mk(asf(w3.x), asf(w3.y), asf(w3.z)), mk(asf(w3.w), asf(w4.x), asf(w4.y)), in_xf);
         } else if ((KM & (1u << K_SPHERE)) && kind == K_SPHERE) {
           sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
-                         asf(w2.y), asf(w2.z), in_xf);
+                         asf(w2.y), asf(w2.z), in_xf, w2.w != 0u);
         } else if ((KM & ((1u << K_TRANSLATE) | (1u << K_YROTATE))) && (kind == K_TRANSLATE || kind == K_YROTATE)) {
           const bool tr = kind == K_TRANSLATE;
           const uint32_t chain = w3.x;   // W_MACRO: fused chain marker
@@ -1193,7 +1194,7 @@ struct MixedTraceK {
             if (rot) rotate_enter(T, r, sn, cs);
             if ((KM & (1u << K_SPHERE)) && g0.x == K_SPHERE)
               sphere_hit<UV>(T, r, h, g0.y, mk(asf(g0.z), asf(g0.w), asf(g1.x)), mk(asf(g1.y), asf(g1.z), asf(g1.w)),
-                             asf(g2.y), asf(g2.z), true);
+                             asf(g2.y), asf(g2.z), true, g2.w != 0u);
             else
               planar_hit(T, r, h, g0.x == K_TRIANGLE, g0.y, mk(asf(g0.z), asf(g0.w), asf(g1.x)), asf(g1.y),
                          mk(asf(g1.z), asf(g1.w), asf(g2.x)), mk(asf(g2.y), asf(g2.z), asf(g2.w)),
@@ -1336,7 +1337,8 @@ struct MixedTraceK {
           const uint4 p0 = bw[0], p1 = bw[1], p2 = bw[2], p3 = bw[3], p4 = bw[4];
           if ((KM & (1u << K_SPHERE)) && p0.x == K_SPHERE) {
             T.tmax = best;
-            sphere_commit<UV>(T, r, h, p0.y, mk(asf(p0.z), asf(p0.w), asf(p1.x)), mk(asf(p1.y), asf(p1.z), asf(p1.w)), asf(p2.z));
+            sphere_commit<UV>(T, r, h, p0.y, mk(asf(p0.z), asf(p0.w), asf(p1.x)), mk(asf(p1.y), asf(p1.z), asf(p1.w)), asf(p2.z),
+                              p2.w != 0u);
           } else {
             // planar_hit's record at t = best (tmax = best: the same plane test accepts it)
             T.tmax = best;

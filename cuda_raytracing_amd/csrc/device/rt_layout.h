@@ -16,7 +16,8 @@ enum : uint32_t {
 // Every scene record becomes one 80-byte node (record indices preserved, WorldRefs resolved).
 // Word layout per kind (w0 = kind, w1 = aux):
 //   BVH      : w1 = left_href | right_href << 16, w2..w7 = x0 x1 y0 y1 z0 z1
-//   SPHERE   : w1 = material, w2..4 centre, w5..7 motion, w8 radius, w9 radius*radius, w10 1/radius
+//   SPHERE   : w1 = material, w2..4 centre, w5..7 motion, w8 radius, w9 radius*radius, w10 1/radius,
+//              w11 = 1 if the material's texture reads u,v (an image texture: the walk computes them)
 //   TRI/QUAD : w1 = material, w2..4 normal, w5 d, w6..8 q, w9..11 u, w12..14 v, w15..17 w
 //   TRANSLATE: w1 = child, w2..4 offset
 //   YROTATE  : w1 = child, w2 sin, w3 cos
@@ -25,7 +26,7 @@ constexpr int kNodeWords = 20;
 enum : int {
   W_KIND = 0, W_AUX = 1,
   W_BOX = 2,
-  W_CENTER = 2, W_MOTION = 5, W_RADIUS = 8, W_RADIUS2 = 9, W_INV_RADIUS = 10,
+  W_CENTER = 2, W_MOTION = 5, W_RADIUS = 8, W_RADIUS2 = 9, W_INV_RADIUS = 10, W_SPHERE_UV = 11,
   W_NORMAL = 2, W_D = 5, W_Q = 6, W_U = 9, W_V = 12, W_W = 15,
   W_OFFSET = 2, W_SIN = 2, W_COS = 3, W_COUNT = 2,
 };

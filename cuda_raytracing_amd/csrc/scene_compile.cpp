@@ -6,6 +6,7 @@
 // texture offset and group range is checked, so malformed bytes are RT_ERR_SCENE instead of a
 // device fault.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <unordered_map>
@@ -319,6 +320,17 @@ int compile_scene(const void *scene_ptr, SceneImage *img) {
   img->stack_need = static_cast<uint32_t>(need);
   auto &W = img->words;
   W = c.nodes;
+  // spheres whose material reads u,v (an image texture, raytracing.cu:332-351): the walk computes the
+  // sphere's u,v only for these (get_sphere_uv's values are read by nothing else); RT_LAZY_UV=0 (A/B): all
+  const char *lz = std::getenv("RT_LAZY_UV");
+  const bool lazy_uv = !(lz && lz[0] == '0');
+  for (uint32_t i = 0; i < sc->hittable_count; ++i) {
+    uint32_t *w = &W[static_cast<size_t>(i) * kNodeWords];
+    if (w[W_KIND] != K_SPHERE) continue;
+    const uint32_t *m = &c.mats[static_cast<size_t>(w[W_AUX]) * kMatWords];
+    const bool textured = m[M_KIND] == MAT_LAMBERTIAN || m[M_KIND] == MAT_DIFFUSE_LIGHT;
+    w[W_SPHERE_UV] = !lazy_uv || (textured && c.texs[static_cast<size_t>(m[M_TEX]) * kTexWords + T_KIND] == T_IMAGE) ? 1u : 0u;
+  }
   img->off_mats = static_cast<uint32_t>(W.size());
   W.insert(W.end(), c.mats.begin(), c.mats.end());
   img->off_texs = static_cast<uint32_t>(W.size());
