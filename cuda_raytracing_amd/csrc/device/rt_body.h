@@ -1045,13 +1045,15 @@ __device__ __forceinline__ bool mix_box(const Trav &T, const SlabRay &R, float x
 
 // candidate value of a quad / triangle (geom_calc_hit, :1060-1077, + the inside test of :1131-1175): the
 // plane t when t >= tmin and the point is inside; ok = false otherwise.  Same operations as planar_hit.
-__device__ __forceinline__ float planar_value(const Ray &r, bool tri, f3 n, float dd, f3 q, f3 uu, f3 vv, f3 ww, bool &ok) {
+// lim: a plane t above it cannot change the walk's result (the caller's bound), so its inside test is skipped
+__device__ __forceinline__ float planar_value(const Ray &r, bool tri, f3 n, float dd, f3 q, f3 uu, f3 vv, f3 ww, bool &ok,
+                                              float lim = __builtin_huge_valf()) {
   ok = false;
   float t = 0.0f;
   const float denom = dot(n, r.d);
   if (fabsf(denom) >= kDenomEps) {
     t = (dd - dot(n, r.o)) / denom;
-    if (kTmin <= t) {
+    if (kTmin <= t && t <= lim) {
       const f3 p = line_at(r.o, t, r.d);
       const f3 pq = sub(p, q);
       const float alpha = dot(ww, cross(pq, vv));
@@ -1154,8 +1156,32 @@ struct MixedTraceK {
         const uint32_t kind = w0.x;
         const bool in_xf = T.tc || T.yc;
         bool expand = false;   // a BVH node whose box passed / a group: push its children (unless a macro)
+        // dispatch: the two common steps (a BVH node; a fused chain ending in a packed sphere) first, every
+        // other kind in one block, so a trip whose lanes hold only common steps skips the rest with one
+        // branch (each divergent `if` costs exec-mask bookkeeping on every trip)
+        const bool xf_kind = kind == K_TRANSLATE || kind == K_YROTATE;
+        constexpr bool packed_chain_ok = (KM & ((1u << K_TRANSLATE) | (1u << K_YROTATE))) && (KM & (1u << K_SPHERE));
+        const bool packed_chain = packed_chain_ok && xf_kind &&
+                                  (w3.x & (kChainFused | kChainPacked)) == (kChainFused | kChainPacked) &&
+                                  (kind == K_TRANSLATE ? T.tc : T.yc) == 0;
+        // translate -> [y-rotate ->] sphere, or y-rotate -> sphere, packed into the head record
+        // (mixed_accel.cpp): the reference's enter, enter, test, cleanup, cleanup steps (:1176-1237) at once
+        auto packed_step = [&](uint4 v0, uint4 v1, uint4 v2, uint4 v3, uint4 v4) {
+          const bool tr = v0.x == K_TRANSLATE;
+          const bool rot = !tr || (v3.x & kChainRotate);
+          const f3 off = mk(asf(v0.z), asf(v0.w), asf(v1.x));
+          const float sn = asf(v3.y), cs = asf(v3.z);
+          if (tr) translate_enter(T, r, off);
+          if (rot) rotate_enter_dir(T, r, sn, cs);   // no box test inside: 1/dir is refreshed at the exit
+          sphere_hit<UV>(T, r, h, v1.y, mk(asf(v1.z), asf(v1.w), asf(v4.x)), mk(asf(v4.y), asf(v4.z), asf(v4.w)),
+                         asf(v2.y), asf(v2.z), true, v2.w != 0u);
+          if (rot) rotate_exit(T, r, h, sn, cs);
+          if (tr) translate_exit(T, r, h, off);
+        };
         if ((KM & (1u << K_BVH)) && kind == K_BVH) {
           expand = box_hit(T, r, asf(w0.z), asf(w0.w), asf(w1.x), asf(w1.y), asf(w1.z), asf(w1.w));
+        } else if (packed_chain) {
+          packed_step(w0, w1, w2, w3, w4);
         } else if ((KM & (1u << K_GROUP)) && kind == K_GROUP) {
           expand = true;
         } else if ((KM & ((1u << K_QUAD) | (1u << K_TRIANGLE))) && (kind == K_QUAD || kind == K_TRIANGLE)) {
@@ -1174,24 +1200,13 @@ struct MixedTraceK {
             const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
             const bool rot = !tr || (chain & kChainRotate);
             float sn = asf(w0.z), cs = asf(w0.w);
-            uint4 g0, g1, g2, g3, g4;
-            if (chain & kChainPacked) {
-              // a sphere chain packed into its head record (mixed_accel.cpp): no dependent loads
-              if (rot) { sn = asf(w3.y); cs = asf(w3.z); }
-              g0 = make_uint4(K_SPHERE, w1.y, w1.z, w1.w);
-              g1 = w4;
-              g2 = w2;
-              g3 = g2; g4 = g2;
-              if (tr) translate_enter(T, r, off);
-            } else {
-              if (tr) {
-                translate_enter(T, r, off);
-                if (rot) { const uint4 c0 = S.w4(w0.y * kNodeWords); sn = asf(c0.z); cs = asf(c0.w); }
-              }
-              const uint32_t gb = (chain & kChainPrimMask) * kNodeWords;
-              g0 = S.w4(gb); g1 = S.w4(gb + 4); g2 = S.w4(gb + 8); g3 = S.w4(gb + 12); g4 = S.w4(gb + 16);
+            if (tr) {
+              translate_enter(T, r, off);
+              if (rot) { const uint4 c0 = S.w4(w0.y * kNodeWords); sn = asf(c0.z); cs = asf(c0.w); }
             }
-            if (rot) rotate_enter(T, r, sn, cs);
+            if (rot) rotate_enter_dir(T, r, sn, cs);   // no box test inside: 1/dir is refreshed at the exit
+            const uint32_t gb = (chain & kChainPrimMask) * kNodeWords;
+            const uint4 g0 = S.w4(gb), g1 = S.w4(gb + 4), g2 = S.w4(gb + 8), g3 = S.w4(gb + 12), g4 = S.w4(gb + 16);
             if ((KM & (1u << K_SPHERE)) && g0.x == K_SPHERE)
               sphere_hit<UV>(T, r, h, g0.y, mk(asf(g0.z), asf(g0.w), asf(g1.x)), mk(asf(g1.y), asf(g1.z), asf(g1.w)),
                              asf(g2.y), asf(g2.z), true, g2.w != 0u);
@@ -1228,7 +1243,7 @@ struct MixedTraceK {
         }
         if (expand) {
           const uint32_t mw = w3.x;   // W_MACRO
-          bool macro = mw != 0;
+          bool macro = (mw & (kMacroStatic | kMacroDynamic)) != 0;
           if (macro) {
             // bounded, finite rays only (finite 1/dir: the slab arithmetic stays monotone, the conservative
             // boxes hold); a dynamic macro only when the ray misses W_XFBOX in the reference's own test
@@ -1293,9 +1308,12 @@ struct MixedTraceK {
           v = sphere_value(r, mk(asf(p0.z), asf(p0.w), asf(p1.x)), mk(asf(p1.y), asf(p1.z), asf(p1.w)), asf(p2.y), ok);
         } else {
           const uint4 p3 = pw[3], p4 = pw[4];
+          // a candidate matters only at or below the running value (best / tie) or below min(second, tin)
+          // (the reach proof reads second only through that minimum): others skip the inside test
           v = planar_value(r, p0.x == K_TRIANGLE, mk(asf(p0.z), asf(p0.w), asf(p1.x)), asf(p1.y),
                            mk(asf(p1.z), asf(p1.w), asf(p2.x)), mk(asf(p2.y), asf(p2.z), asf(p2.w)),
-                           mk(asf(p3.x), asf(p3.y), asf(p3.z)), mk(asf(p3.w), asf(p4.x), asf(p4.y)), ok);
+                           mk(asf(p3.x), asf(p3.y), asf(p3.z)), mk(asf(p3.w), asf(p4.x), asf(p4.y)), ok,
+                           fmaxf(cur_k, fminf(second, tin)));
         }
         if (ok) {
           const uint32_t g = pw[5].x;   // MP_GROUP

@@ -326,6 +326,9 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     // node words, which every other traversal ignores)
     const char *m = std::getenv("RT_MIXED");
     if (!c->accel_ok && !(m && m[0] == '0') && rt::build_mixed_accel(&c->img, &c->mixed, &why)) c->mixed_ok = true;
+    if (c->mixed_ok && std::getenv("RT_DEBUG"))
+      std::fprintf(stderr, "[rt] mixed accel: %u macros (%u dynamic), %u packed sphere chains\n", c->mixed.macros,
+                   c->mixed.dynamic, c->mixed.packed);
   }
   std::vector<uint32_t> dev_words = c->img.words;
   if (c->accel_ok) {
