@@ -1718,16 +1718,18 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     uint32_t nhot = sparse ? static_cast<uint32_t>(__popcll(__ballot(busy && hot))) : 0u;
     while (m != 0 && !exhausted) {
       if (chunk_pos >= chunk_end) {
-        if (sparse && (nhot >= A.prio_lanes || (nhot > 0 && prio_done))) break;
+        if (sparse && !A.prio_mix && (nhot >= A.prio_lanes || (nhot > 0 && prio_done))) break;
         // the costliest tiles (the first prio_ids ids of the longest-first order) may be handed out in
         // prio_chunk-pixel pieces from their own counter, so that their long pixel chains spread over
-        // more waves; every other tile goes out whole
+        // more waves; every other tile goes out whole.  Mixed (A.prio_mix): a wave holding prio_lanes of
+        // those pixels takes ordinary tiles for its other lanes meanwhile.
         uint32_t base = 0, size = static_cast<uint32_t>(kChunk), hold = 0;
-        const bool split = A.prio_chunk < static_cast<uint32_t>(kChunk) && !prio_done;
+        const bool capped = A.prio_mix && nhot >= A.prio_lanes;
+        const bool split = A.prio_chunk < static_cast<uint32_t>(kChunk) && !prio_done && !capped;
         if (lane == 0) {
           if (split) base = atomicAdd(A.work + 1, A.prio_chunk);
           if (!split || base >= A.prio_ids) {
-            if (sparse && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
+            if (sparse && !A.prio_mix && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
             else base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
           } else {
             size = A.prio_chunk;
@@ -1736,9 +1738,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
         size = __builtin_amdgcn_readfirstlane(__shfl(size, 0));
         hold = __builtin_amdgcn_readfirstlane(__shfl(hold, 0));
-        if (size == static_cast<uint32_t>(kChunk)) prio_done = true;
+        if (size == static_cast<uint32_t>(kChunk) && !capped) prio_done = true;
         if (hold) break;
-        if (base >= A.n_ids) { exhausted = true; break; }
+        // a capped mixed wave that finds the ordinary tiles gone waits for a hot lane to free (costly
+        // pixels may still be queued); the queue is exhausted only when both counters are drained
+        if (base >= A.n_ids) { if (!capped) exhausted = true; break; }
         if (A.reverse_tiles) base = A.n_ids - kChunk - base;   // whole tiles: n_ids is a multiple of 64
         tiles_taken++;
         chunk_pos = base;

@@ -200,6 +200,7 @@ struct RenderArgs {
                                   // the longest-first order) run their wave at raised issue priority
   uint32_t prio_chunk;            // < 64: those ids are handed out in pieces of this many (work[1])
   uint32_t prio_lanes;            // < 64: a wave holds at most this many of them and nothing else meanwhile
+  uint32_t prio_mix;              // with prio_lanes < 64: the wave's other lanes take ordinary tiles meanwhile
   uint32_t defer_lanes;           // the round's rejection stops once at most this many lanes of the
                                   // wave still need a try (they resume next round; 0 = never early)
   uint32_t black_skip;            // every attenuation is finite (host-checked): a path ending in

@@ -74,6 +74,7 @@ constexpr size_t kLdsReserve = 1024;           // per resident block, see the co
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
+constexpr int kMixLanes = 32;                   // mixed hot waves (verified mixed walk): costly pixels per wave
 constexpr uint32_t kRcLdsMaxLevels = 256;  // colour-stack levels kept in LDS at most (max_bounces is a u8)
 
 // LDS bytes of one colour-stack level for a 256-thread block: 32-bit codes, or 16-bit in narrow kernels
@@ -177,6 +178,8 @@ struct rt_context {
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
   int prio_chunk = -1;                          // RT_PRIO_CHUNK: those tiles handed out in pieces of this many pixels
   int prio_lanes = 0;                           // RT_PRIO_LANES: waves holding them keep at most this many lanes busy
+  int prio_mix = -1;                            // RT_PRIO_MIX=1/0: ... and fill their other lanes with ordinary
+                                                // tiles (-1: the default, on for the verified mixed walk)
                                                 // (0: the default, kSparseLanes on noise scenes; 64: off)
                                                 // (-1 auto: 1 with cooperative noise, else whole tiles)
   uint32_t coop_noise = 32;                     // RT_COOP_NOISE: cooperative noise octaves when <= this many lanes
@@ -305,6 +308,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
   if (const char *e = std::getenv("RT_PRIO_LANES")) c->prio_lanes = std::atoi(e);
+  if (const char *e = std::getenv("RT_PRIO_MIX")) c->prio_mix = e[0] == '1' ? 1 : 0;
   if (const char *e = std::getenv("RT_COOP_NOISE")) c->coop_noise = static_cast<uint32_t>(std::min(32, std::max(0, std::atoi(e))));
   if (const char *e = std::getenv("RT_PRIO_CHUNK")) {
     const int v = std::atoi(e);
@@ -665,6 +669,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.trace_min_iters = c->trace_min_iters;
   a.prio_chunk = 64u;   // whole tiles unless the longest-first schedule splits its costliest ones
   a.prio_lanes = 64u;   // no sparse waves (the probe launch keeps these defaults)
+  a.prio_mix = 0u;
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;
@@ -709,25 +714,33 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), s) != hipSuccess)
       return RT_ERR_HIP;
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
-    // noise scenes: sparse hot waves (below) by default, over the 16 costliest tiles
-    const bool noise_sched = c->img.has_noise && c->coop_noise;
-    const int lanes_hot = c->prio_lanes != 0 ? c->prio_lanes : (noise_sched ? kSparseLanes : 0);
-    const int pt = c->prio_tiles >= 0 ? c->prio_tiles : ((lanes_hot > 0 && lanes_hot < 64) ? kSparseTiles : kPrioTiles);
+    // noise scenes: sparse hot waves (below) by default, over the 16 costliest tiles; the verified mixed
+    // walk: mixed hot waves over the costliest quarter of the tiles (below)
+    const bool mix_sched = c->prio_mix == 1 || (c->prio_mix < 0 && c->used_traversal == RT_TRAV_MIXED);
+    const bool noise_sched = c->img.has_noise && c->coop_noise && !mix_sched;
+    const int lanes_hot = c->prio_lanes != 0 ? c->prio_lanes : (mix_sched ? kMixLanes : noise_sched ? kSparseLanes : 0);
+    const int pt = c->prio_tiles >= 0 ? c->prio_tiles
+                                      : mix_sched ? static_cast<int>(std::max<uint32_t>(n_tiles / 4u, kSparseTiles))
+                                      : ((lanes_hot > 0 && lanes_hot < 64) ? kSparseTiles : kPrioTiles);
     a.prio_ids = static_cast<uint32_t>(std::min<uint64_t>(static_cast<uint64_t>(pt) * 64u, a.n_ids));
     // The costliest tiles of a noise scene hold pixels whose paths are trapped between noise surfaces
     // (the Perlin scene's contact point: ~35k serial rounds per pixel); handed out one pixel at a time
     // they spread over many waves, each with few noise lanes, whose octaves the idle lanes then share
     // (measured on scene 17, d50, spp 1024: 204 ms whole tiles without cooperation, 168 with, 135 with
     // single pixels; scene 0 and Cornell lose 4-10 % with split tiles, so they keep whole tiles)
-    const int pcn = c->prio_chunk >= 0 ? c->prio_chunk : (noise_sched ? 1 : 64);
+    const int pcn = c->prio_chunk >= 0 ? c->prio_chunk : ((noise_sched || mix_sched) ? 1 : 64);
     a.prio_chunk = a.prio_ids ? static_cast<uint32_t>(pcn) : 64u;
     // Sparse hot waves: a wave holding pixels of those tiles keeps at most lanes_hot of them busy and takes
     // no other pixel meanwhile, so the trapped chains run in waves with few divergent lanes (and issue
     // priority) for the whole frame, not only once the rest is done (single-pixel hand-out).  Scene 17:
     // 135-139 -> 99-101 ms per frame, scene 19: 205 -> 165; scene 0 +12 %, Cornell +5 %, 10k +-3 %, so
     // noise scenes only (profiles/r03_ab_sparse_hot_waves_*.jsonl).  RT_PRIO_LANES=64 turns it off.
+    // Mixed hot waves: the same cap, but the wave's other lanes take ordinary tiles meanwhile, so the
+    // costliest pixels start at once, spread over every wave, and their walks share trips with cheap
+    // pixels (the paused walk lets those finish their samples meanwhile).  final_scene: see DESIGN §2.
     if (a.prio_ids && lanes_hot > 0 && lanes_hot < 64) {
       a.prio_lanes = static_cast<uint32_t>(lanes_hot);
+      a.prio_mix = mix_sched ? 1u : 0u;
       a.prio_chunk = 1u;
     }
   }

@@ -828,7 +828,9 @@ def test_mixed_walk_fallback_path_vs_oracle(monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"RT_DEFER_TRACE": "64", "RT_TRACE_MIN": "1"}, {"RT_MIX_PAUSE": "0"},
-                                 {"RT_MIX_PACK": "0"}, {"RT_MIX_PAUSE": "0", "RT_MIX_PACK": "0"}])
+                                 {"RT_MIX_PACK": "0"}, {"RT_MIX_PAUSE": "0", "RT_MIX_PACK": "0"},
+                                 {"RT_PRIO_MIX": "1", "RT_PRIO_LANES": "4", "RT_PRIO_TILES": "8"},
+                                 {"RT_PRIO_MIX": "1", "RT_PRIO_LANES": "2", "RT_PRIO_TILES": "100000"}])
 def test_mixed_walk_pause_and_packed_chains(monkeypatch, env):
     # the walk paused between reference steps (forced early: any round with <= 1/4 of its walkers left)
     # and sphere chains packed into their head records, each on and off, vs the oracle
