@@ -210,6 +210,8 @@ struct RenderArgs {
   uint32_t mix_nodes, mix_prims;  // verified mixed-world traversal: word offsets of its SAH nodes / prims
   uint32_t *mix_fallbacks;        // macro walks it handed back to the reference walk (diagnostic)
   uint32_t mix_no_proof;          // test aid (RT_MIX_PROVE=0): every macro walk takes the fallback
+  uint32_t tail_prio;             // queue drained: a wave's issue priority grows with the samples its least
+                                  // advanced pixel has left (the frame ends with its longest chain)
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

@@ -177,6 +177,7 @@ struct rt_context {
   uint32_t max_tries = 0;                       // RT_MAX_TRIES: rejection tries per round (0 = unlimited)
   int prio_tiles = -1;                          // RT_PRIO_TILES: costliest tiles run at raised priority (-1 auto)
   int prio_chunk = -1;                          // RT_PRIO_CHUNK: those tiles handed out in pieces of this many pixels
+  int tail_prio = -1;                           // RT_TAIL_PRIO: tail issue priority by remaining samples (-1: auto)
   int prio_lanes = 0;                           // RT_PRIO_LANES: waves holding them keep at most this many lanes busy
   int prio_mix = -1;                            // RT_PRIO_MIX=1/0: ... and fill their other lanes with ordinary
                                                 // tiles (-1: the default, on for the verified mixed walk)
@@ -308,6 +309,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_PRIO_TILES")) c->prio_tiles = std::atoi(e);
   if (const char *e = std::getenv("RT_PRIO_LANES")) c->prio_lanes = std::atoi(e);
+  if (const char *e = std::getenv("RT_TAIL_PRIO")) c->tail_prio = e[0] == '1' ? 1 : 0;
   if (const char *e = std::getenv("RT_PRIO_MIX")) c->prio_mix = e[0] == '1' ? 1 : 0;
   if (const char *e = std::getenv("RT_COOP_NOISE")) c->coop_noise = static_cast<uint32_t>(std::min(32, std::max(0, std::atoi(e))));
   if (const char *e = std::getenv("RT_PRIO_CHUNK")) {
@@ -670,6 +672,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.prio_chunk = 64u;   // whole tiles unless the longest-first schedule splits its costliest ones
   a.prio_lanes = 64u;   // no sparse waves (the probe launch keeps these defaults)
   a.prio_mix = 0u;
+  a.tail_prio = 0u;   // the probe launch keeps it off
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;
@@ -744,6 +747,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
       a.prio_chunk = 1u;
     }
   }
+  // Tail issue priority: on for the verified mixed walk (final_scene 800x800 spp 64: 638-649 -> 598-611 ms
+  // per frame), within noise elsewhere (scene 0 -1 %, 10k +1 %; profiles/r03_ab_tail_prio.jsonl)
+  a.tail_prio = (c->tail_prio == 1 || (c->tail_prio < 0 && c->used_traversal == RT_TRAV_MIXED)) ? 1u : 0u;
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);

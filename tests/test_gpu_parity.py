@@ -227,6 +227,20 @@ def test_tile_schedules_agree(sched, monkeypatch):
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
 
 
+@pytest.mark.parametrize("idx,W,H,spp", [(0, 96, 54, 24), (20, 64, 36, 16), (3, 48, 48, 16), (17, 64, 36, 16)])
+@pytest.mark.parametrize("tail", ["0", "1"])
+def test_tail_issue_priority_agrees(idx, W, H, spp, tail, monkeypatch):
+    # RT_TAIL_PRIO only reorders the SIMD's issue once the queue is drained: frames stay oracle-exact on every
+    # traversal it can run under (static, verified sphere walk, verified mixed walk, noise scenes)
+    monkeypatch.setenv("RT_TAIL_PRIO", tail)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=16)
+    fb, _ = gpu(w.scene(), cam, p)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+
+
 @pytest.mark.parametrize("idx", [0, 1, 2, 8, 13, 18, 19])
 def test_folded_and_unfolded_static_traversal(idx):
     # exact constant folding of primitive tests (scene_codegen.cpp) must not change a single bit
@@ -348,15 +362,30 @@ def test_verified_sphere_traversal_matches_oracle(idx, W, H, spp):
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
 
 
+def _rows_match_oracle(w, s, cam, W, H, spp, b, full, stride):
+    """Rows 0, stride, 2*stride, ... of a GPU frame against the oracle's render of exactly those rows (the RNG
+    subsequence is the global pixel index, so a row subset is comparable)."""
+    n = (H - 1) // stride + 1
+    p = rt.make_params(s, W, H, spp=spp, bounces=b, row_offset=0, row_stride=stride, row_count=n)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    got = full[0::stride]
+    assert got.shape == ref.shape
+    bad = np.argwhere(bits(got) != bits(ref))
+    assert bad.size == 0, f"{len(bad)} values differ vs the oracle, first at row {bad[0][0] * stride} col {bad[0][1]}"
+
+
 @pytest.mark.parametrize("idx,W,H,spp,b", [(20, 480, 270, 16, 16), (2, 480, 270, 16, 50)])
 def test_verified_sphere_traversal_matches_reference_walk_large(idx, W, H, spp, b):
-    # millions of rays: the verified walk against the reference walk on the GPU (itself oracle-exact)
+    # millions of rays: the verified walk against the reference walk on the GPU (itself oracle-exact), and
+    # every 7th row of the verified walk's frame against the oracle itself
     w, s = rt.build_scene(idx)
     cam, W, H = rt.camera_from_settings(s, W, H)
     a, sa = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_ACCEL))
     c, sc = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_LANE))
     assert sa.traversal == rt.RT_TRAV_ACCEL and sc.traversal == rt.RT_TRAV_LANE
     assert np.array_equal(bits(a), bits(c))
+    _rows_match_oracle(w, s, cam, W, H, spp, b, a, 7)
 
 
 @pytest.mark.parametrize("idx,W,H,spp,b", [(0, 480, 270, 16, 16), (1, 320, 320, 8, 50), (17, 480, 270, 8, 50),
@@ -371,6 +400,7 @@ def test_static_fast_paths_match_reference_walk_large(idx, W, H, spp, b):
     c, sc = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=spp, bounces=b, flags=rt.RT_FLAG_FORCE_LANE | rt.RT_FLAG_NO_JIT))
     assert sa.traversal == rt.RT_TRAV_STATIC and sa.folded == 1 and sc.traversal == rt.RT_TRAV_LANE
     assert np.array_equal(bits(a), bits(c))
+    _rows_match_oracle(w, s, cam, W, H, spp, b, a, 7)   # and every 7th row of it against the oracle
 
 
 def _uniforms_from_states(st: np.ndarray, n: int) -> np.ndarray:
