@@ -329,11 +329,15 @@ std::string jit_lane_source(const SceneImage &img, int variant) {
   return src;
 }
 
-std::string jit_accel_source(const SceneImage &img, int variant) {
+std::string waves_attr_n(int waves) {
+  return waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : waves_attr();
+}
+
+std::string jit_accel_source(const SceneImage &img, int variant, int waves) {
   const int v = variant & kJitVarMask;
   const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u>";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
-  src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr() + " void rt_accel_render(RenderArgs A) {\n  render_body<" +
+  src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr_n(waves) + " void rt_accel_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarNoProbe) + ", " + at + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_accel_render_count(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarCount | kVarNoProbe) + ", " + at + ">(A);\n}\n";
@@ -343,14 +347,14 @@ std::string jit_accel_source(const SceneImage &img, int variant) {
   return src;
 }
 
-std::string jit_mixed_source(const SceneImage &img, int variant) {
+std::string jit_mixed_source(const SceneImage &img, int variant, int waves) {
   const int v = variant & kJitVarMask;
   // pausable walk (RT_MIX_PAUSE=0: the round waits for every walk, A/B)
   const char *pe = std::getenv("RT_MIX_PAUSE");
   const bool pause = !(pe && pe[0] == '0');
   const std::string mt = "MixedTraceK<" + std::to_string(scene_kinds(img)) + "u, " + (pause ? "true" : "false") + ">";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
-  src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr() + " void rt_mixed_render(RenderArgs A) {\n  render_body<" +
+  src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr_n(waves) + " void rt_mixed_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarNoProbe) + ", " + mt + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_mixed_render_count(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarCount | kVarNoProbe) + ", " + mt + ">(A);\n}\n";
@@ -360,16 +364,63 @@ std::string jit_mixed_source(const SceneImage &img, int variant) {
   return src;
 }
 
+// One residency step for a few registers: the allocator often lands just above a boundary of the hardware's
+// 16-VGPR granule (the 10k walk at 82 VGPRs = 5 waves/SIMD, 80 would be 6; the mixed walk at 98 = 4, 96 would
+// be 5).  When the render kernel is within kRaiseSlack VGPRs of the next residency, its module is rebuilt
+// with amdgpu_waves_per_eu(that residency) and kept if the kernel then reaches it with no scratch.
+// RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves the first build.
+constexpr int kRaiseSlack = 4;
+
+int render_vgprs(hipFunction_t fn, int *scratch) {
+  int v = 0, sc = 0;
+  if (hipFuncGetAttribute(&v, HIP_FUNC_ATTRIBUTE_NUM_REGS, fn) != hipSuccess) v = 0;
+  if (hipFuncGetAttribute(&sc, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, fn) != hipSuccess) sc = -1;
+  *scratch = sc;
+  return v;
+}
+
+template <class Source>
+void raise_residency(const Source &source, const char *prefix, JitKernels *out) {
+  if (std::getenv("RT_JIT_WAVES")) return;
+  if (const char *e = std::getenv("RT_JIT_RAISE")) if (e[0] == '0') return;
+  int sc0 = 0;
+  const int v0 = render_vgprs(out->render, &sc0);
+  if (v0 <= 0 || sc0 != 0) return;
+  const int cur = resident_blocks_by_vgprs(v0);
+  for (int w = cur + 1; w <= 8; ++w) {
+    const int limit = 512 / w / 8 * 8;   // the allocator's budget for w waves (granule 8)
+    if (resident_blocks_by_vgprs(limit) <= cur) continue;
+    if (v0 - limit > kRaiseSlack) return;
+    JitKernels k = *out;
+    std::string why;
+    if (!build_module(source(w), prefix, &k, &why)) return;
+    int sc = 0;
+    const int v = render_vgprs(k.render, &sc);
+    if (std::getenv("RT_DEBUG"))
+      std::fprintf(stderr, "[rt] jit residency raise %s: %d VGPRs (%d/CU) -> waves_per_eu(%d): %d VGPRs, scratch %d B\n",
+                   prefix, v0, cur, w, v, sc);
+    if (v > 0 && sc == 0 && resident_blocks_by_vgprs(v) > cur) {
+      k.ms += out->ms;
+      *out = k;
+    }
+    return;
+  }
+}
+
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
-  return build_module(jit_mixed_source(img, variant), "rt_mixed", out, why);
+  if (!build_module(jit_mixed_source(img, variant), "rt_mixed", out, why)) return false;
+  raise_residency([&](int w) { return jit_mixed_source(img, variant, w); }, "rt_mixed", out);
+  return true;
 }
 
 bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
-  return build_module(jit_accel_source(img, variant), "rt_accel", out, why);
+  if (!build_module(jit_accel_source(img, variant), "rt_accel", out, why)) return false;
+  raise_residency([&](int w) { return jit_accel_source(img, variant, w); }, "rt_accel", out);
+  return true;
 }
 
 bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {

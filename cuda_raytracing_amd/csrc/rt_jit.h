@@ -37,10 +37,10 @@ bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::
 std::string jit_lane_source(const SceneImage &img, int variant);
 // Verified sphere traversal kernels (AccelTraceK over the scene's node kinds for the fallback walk).
 bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
-std::string jit_accel_source(const SceneImage &img, int variant);
+std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0);   // waves > 0: amdgpu_waves_per_eu
 // verified mixed-world traversal kernels (MixedTraceK over the scene's node kinds)
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
-std::string jit_mixed_source(const SceneImage &img, int variant);
+std::string jit_mixed_source(const SceneImage &img, int variant, int waves = 0);
 uint32_t scene_kinds(const SceneImage &img);
 // material / texture kinds present, as variant bits (kVarMatShift / kVarTexShift)
 int scene_shading_bits(const SceneImage &img);
