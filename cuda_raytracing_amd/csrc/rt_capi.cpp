@@ -939,7 +939,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     rt::SphereAccel a;
     std::string why;
     if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
-    src = rt::jit_accel_source(img, variant);
+    src = rt::jit_accel_source(img, variant, rt::accel_waves());
   } else if (traversal == RT_TRAV_MIXED) {
     rt::MixedAccel m;
     std::string why;

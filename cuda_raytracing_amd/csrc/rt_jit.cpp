@@ -415,11 +415,22 @@ bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std:
   return true;
 }
 
+// The verified sphere walk is latency-bound (dependent node loads): hipRTC allocates its render kernel
+// ~97 VGPRs (4 waves/SIMD); asked for 6 waves (80 VGPRs) it runs the 10k frame 226-231 -> 206-208 ms
+// (profiles/r03_ab_jit_waves.jsonl).  RT_ACCEL_WAVES=N overrides (0: the allocator's own choice);
+// RT_JIT_WAVES, when set, applies to every run-time kernel instead.
+int accel_waves() {
+  if (std::getenv("RT_JIT_WAVES")) return 0;
+  if (const char *e = std::getenv("RT_ACCEL_WAVES")) return std::max(0, std::min(8, std::atoi(e)));
+  return 6;
+}
+
 bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
-  if (!build_module(jit_accel_source(img, variant), "rt_accel", out, why)) return false;
-  raise_residency([&](int w) { return jit_accel_source(img, variant, w); }, "rt_accel", out);
+  const int w = accel_waves();
+  if (!build_module(jit_accel_source(img, variant, w), "rt_accel", out, why)) return false;
+  if (w == 0) raise_residency([&](int n) { return jit_accel_source(img, variant, n); }, "rt_accel", out);
   return true;
 }
 
