@@ -22,8 +22,10 @@ reference render() region, cold and warm code-object cache), `cpu_baseline` (the
 -O3 -march=native on this host, all cores and 1 core, on a bounded row sample whose GPU render is
 compared bit for bit).
 roofline: VALU-bound kernel; achieved = algorithmic FP32 ops per render launch (op model of SURVEY §8d
-on this workload's measured per-sample visit counts) / the render kernel's median HIP-event duration
-over the timed frames (events on the launch stream; rocprofv3 sees the same launches).
+on this workload's measured per-sample visit counts) / the render kernel's median duration over the timed
+frames, measured by the kernel itself (first wave start to last wave end on the device's s_memrealtime wall
+clock, rt_stats.render_kernel_ms — what rocprofv3 reports as the kernel's duration; the stream-event window
+around the launch is reported beside it).
 """
 from __future__ import annotations
 
@@ -393,7 +395,8 @@ def main():
     elapsed, fstats = timed(args.steps, 1)
     value = samples_per_step * args.steps / elapsed / 1e6
     med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
-    render_ms = med([st.render_ms for st in fstats])
+    render_ms = med([st.render_kernel_ms if st.render_kernel_ms > 0 else st.render_ms for st in fstats])
+    render_event_ms = med([st.render_ms for st in fstats])
     seed_ms = med([st.init_ms for st in fstats])
     sched_ms = med([st.sched_ms for st in fstats])
     achieved = ops_per_sample * local_samples / (render_ms / 1e3) / 1e12
@@ -460,7 +463,8 @@ def main():
                            rt.RT_TRAV_MIXED: "rt_mixed_render (hipRTC)"}.get(
                     cst.traversal, "rt_lane_render (hipRTC)"),
             },
-            "kernel_ms": {"render_median": round(render_ms, 3), "seed_median": round(seed_ms, 3),
+            "kernel_ms": {"render_median": round(render_ms, 3), "render_event_median": round(render_event_ms, 3),
+                          "seed_median": round(seed_ms, 3),
                           "schedule_median": round(sched_ms, 3),
                           "render_only_msamples_s": round(local_samples / (render_ms / 1e3) / 1e6, 1)},
             "pipelined": pipelined,
@@ -479,7 +483,8 @@ def main():
                     "frac": round(exec_ops * local_samples / (render_ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 4),
                     "note": "verified SAH walk's executed node visits (2 boxes each) and leaf tests instead of the "
                             "reference tree's visits"},
-                "measured_on": "median render-kernel HIP-event duration over the timed frames (launch stream)",
+                "measured_on": "median render-kernel duration over the timed frames, from the kernel's own first-wave-start "
+                               "to last-wave-end s_memrealtime stamps (rt_stats.render_kernel_ms)",
                 "counters_per_sample": {k: round(v / max(counters["samples"], 1), 4) for k, v in counters.items()
                                         if k not in ("samples", "max_stack", "stack_overflow", "rng_draws")},
             },

@@ -25,6 +25,7 @@ __all__ = [
     "RT_FLAG_NO_JIT", "RT_FLAG_RC_AUDIT", "RT_FLAG_FORCE_MIXED", "RT_FLAG_NO_MIXED", "RT_TRAV_MIXED", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_FLAG_FORCE_ACCEL", "RT_FLAG_NO_ACCEL", "RT_TRAV_ACCEL", "RT_TRAV_LANE",
     "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "accel_build", "tonemap_device", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError", "load_image",
+    "render_devices", "multi_row_map",
 ]
 
 
@@ -259,6 +260,29 @@ def render(scene: Scene, camera: Camera, params: Params, with_stats: bool = Fals
     _check(_abi.hip_lib().rt_render(C.byref(scene), C.byref(camera), C.byref(params),
                                     out.ctypes.data_as(C.c_void_p), C.byref(st)), "rt_render")
     return (out, st) if with_stats else out
+
+
+def render_devices(scene: Scene, camera: Camera, params: Params, devices, rgb: bool = True, ppm: bool = True,
+                   with_stats: bool = False):
+    """One process, several devices (rt_render_devices): rows dealt round-robin over `devices`, one RCCL gather
+    to devices[0], un-permuted there.  Returns (float32 [rows, W, 3] or None, uint8 [rows, W, 3] or None[, Stats])."""
+    devs = (C.c_int * len(devices))(*devices)
+    shape = (params.row_count, params.width, 3)
+    f = np.zeros(shape, dtype=np.float32) if rgb else None
+    b = np.zeros(shape, dtype=np.uint8) if ppm else None
+    st = Stats()
+    _check(_abi.hip_lib().rt_render_devices(C.byref(scene), C.byref(camera), C.byref(params), devs, len(devices),
+                                            None if f is None else f.ctypes.data_as(C.c_void_p),
+                                            None if b is None else b.ctypes.data_as(C.c_void_p), C.byref(st)),
+           "rt_render_devices")
+    return (f, b, st) if with_stats else (f, b)
+
+
+def multi_row_map(row_count: int, n_devices: int, k: int):
+    """rt_multi_row_map: (device, row in its shard, that shard's rows, longest shard) of frame row k."""
+    o = [C.c_int32() for _ in range(4)]
+    _check(_abi.hip_lib().rt_multi_row_map(row_count, n_devices, k, *(C.byref(x) for x in o)), "rt_multi_row_map")
+    return tuple(x.value for x in o)
 
 
 class RenderContext:

@@ -100,6 +100,7 @@ class Stats(C.Structure):
         ("accel_fallbacks", C.c_uint32), ("jit_source", C.c_int32), ("jit_ms", C.c_double),
         ("rc_hbm_slots", C.c_uint64), ("rc_lds_levels", C.c_int32), ("mix_macros", C.c_int32),
         ("mix_fallbacks", C.c_uint32), ("pad_", C.c_int32),
+        ("render_kernel_ms", C.c_double), ("gather_ms", C.c_double), ("devices", C.c_int32), ("pad2_", C.c_int32),
     ]
 
     def counter_dict(self):
@@ -175,7 +176,8 @@ def host_lib():
 HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_context_render_ppm", "rt_context_timing",
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
-               "rt_seed_states", "rt_kernel_source", "rt_mixed_build"]
+               "rt_seed_states", "rt_kernel_source", "rt_mixed_build", "rt_multi_create", "rt_multi_render",
+               "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map"]
 
 
 def _bind_single_hip_runtime():
@@ -222,6 +224,13 @@ def hip_lib():
         _sig(L.rt_mixed_build, C.c_int, C.POINTER(Scene), C.POINTER(C.c_uint32))
         _sig(L.rt_seed_states, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_kernel_source, C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.c_char_p, C.c_uint64)
+        _sig(L.rt_multi_create, C.c_int, C.POINTER(Scene), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p))
+        _sig(L.rt_multi_render, C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P, C.POINTER(Stats))
+        _sig(L.rt_multi_destroy, None, P)
+        _sig(L.rt_render_devices, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), C.POINTER(C.c_int),
+             C.c_int, P, P, C.POINTER(Stats))
+        i32p = C.POINTER(C.c_int32)
+        _sig(L.rt_multi_row_map, C.c_int, C.c_int32, C.c_int32, C.c_int32, i32p, i32p, i32p, i32p)
         _hip = L
     return _hip
 

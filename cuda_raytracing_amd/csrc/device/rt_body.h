@@ -1569,6 +1569,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const bool probe = (F & kVarProbe) != 0 || ((F & kVarNoProbe) == 0 && A.probe_cost != nullptr);
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
+  const uint64_t t_wave0 = __builtin_amdgcn_s_memrealtime();   // kernel-only span (A.span)
   Mem<LDS> S{A.scene};
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
@@ -2080,6 +2081,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
   }
 
+  if (A.span && lane == 0) {   // vector atomics from one lane per wave: first start, last end of the launch
+    atomicMax(A.span, static_cast<unsigned long long>(~t_wave0));
+    atomicMax(A.span + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
+  }
   if (TRACE && A.wave_trace && lane == 0) {
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
     const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID

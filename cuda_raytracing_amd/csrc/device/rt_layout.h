@@ -212,6 +212,10 @@ struct RenderArgs {
   uint32_t mix_no_proof;          // test aid (RT_MIX_PROVE=0): every macro walk takes the fallback
   uint32_t tail_prio;             // queue drained: a wave's issue priority grows with the samples its least
                                   // advanced pixel has left (the frame ends with its longest chain)
+  // kernel-only timing (non-null on the render launch): span[0] = max over waves of ~start, span[1] = max of
+  // end, s_memrealtime ticks (the device's wall clock) — the launch's first wave start to its last wave end,
+  // like a profiler's kernel duration and unlike stream events, never widened by neighbouring work
+  unsigned long long *span;
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

@@ -1,11 +1,12 @@
 // cli.cpp — `raytracing`, the reference's command-line surface (main.cu:29-131) on the MI355X path.
 //
-//   raytracing [scene] [sN|bN] [sN|bN] [wN] [hN]
+//   raytracing [scene] [sN|bN] [sN|bN] [wN] [hN] [gN]
 //
 // argv[1] selects a catalog scene (main.cu:52-117, plus 20 = random 10k spheres); 'sN' sets samples per
 // pixel, 'bN' max bounces (main.cu:118-129).  Additive flags: 'wN'/'hN' override the resolution (the
-// reference derives H = (int)(W / ratio), raytracing.cu:1659-1660).  The device is HIP's current one
-// (select with HIP_VISIBLE_DEVICES).
+// reference derives H = (int)(W / ratio), raytracing.cu:1659-1660); 'gN' renders on the first N visible
+// devices (rows interleaved, one RCCL gather: rt_render_devices).  Without 'gN' the device is HIP's current
+// one (select with HIP_VISIBLE_DEVICES).
 // Writes settings.img_name as binary P6 PPM into the current directory, like render() (:1772).
 #include <chrono>
 #include <cstdio>
@@ -27,7 +28,7 @@ int main(int argc, char **argv) {
     rt_world_destroy(w);
     return 1;
   }
-  int32_t width = 0, height = 0;
+  int32_t width = 0, height = 0, gpus = 0;
   for (int a = 2; a < argc; ++a) {
     const char *v = argv[a] + 1;
     switch (argv[a][0]) {
@@ -35,6 +36,7 @@ int main(int argc, char **argv) {
       case 's': s.samples_per_pixel = std::atoi(v); break;
       case 'w': width = std::atoi(v); break;
       case 'h': height = std::atoi(v); break;
+      case 'g': gpus = std::atoi(v); break;
       default: break;
     }
   }
@@ -59,7 +61,13 @@ int main(int argc, char **argv) {
   p.background = s.background; p.seed = 1234; p.flags = 0;
   std::vector<float> fb(static_cast<size_t>(W) * H * 3);
   rt_stats stats;
-  st = rt_render(&sc, &cam, &p, fb.data(), &stats);
+  if (gpus > 0) {   // one process, N devices (rt_multi.cpp): the float rows are gathered for pixels_to_ppm
+    std::vector<int> devs(gpus);
+    for (int g = 0; g < gpus; ++g) devs[g] = g;
+    st = rt_render_devices(&sc, &cam, &p, devs.data(), gpus, fb.data(), nullptr, &stats);
+  } else {
+    st = rt_render(&sc, &cam, &p, fb.data(), &stats);
+  }
   std::printf("rt_render status: %s\n", rt_status_string(st));
   if (st != RT_OK) {
     rt_world_destroy(w);
@@ -69,6 +77,7 @@ int main(int argc, char **argv) {
   std::printf("Rendering time: %fs\n", stats.render_ms / 1e3);
   std::printf("RNG seeding time: %fms, end-to-end: %fms, %.1f Msamples/s\n", stats.init_ms, stats.total_ms,
               static_cast<double>(stats.samples) / (stats.render_ms * 1e3));
+  if (gpus > 0) std::printf("Devices: %d, RCCL gather + un-permute: %fms\n", stats.devices, stats.gather_ms);
   if (rt_write_ppm(s.img_name, fb.data(), static_cast<uint32_t>(W), static_cast<uint32_t>(H)) != RT_OK)
     std::fprintf(stderr, "Couldn't open the file for writing\n");
   const double e2e = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();

@@ -2,12 +2,13 @@
 //
 // make_image_texture (raytracing.cu:332-341) loads its file with stbi_loadf from the third-party
 // stb_image v2.30 that the reference vendors (include/stb_image.h); the catalog's earth texture is a
-// JPEG (:2043, :2180).  This is a decoder written for this project from the JPEG standard (ITU-T T.81:
-// baseline and extended sequential Huffman, progressive with spectral selection and successive
-// approximation, restart intervals, 1/3/4 components, any integer sampling factors up to 4), with the
-// numerical choices stb_image v2.30 makes wherever the standard leaves them open, so that the texels
-// are the same bits (tests/test_image_load.py compares against stb_image itself, compiled from the
-// reference tree into oracle/_ref):
+// JPEG (:2043, :2180).  This decoder (ITU-T T.81: baseline and extended sequential Huffman, progressive
+// with spectral selection and successive approximation, restart intervals, 1/3/4 components, any integer
+// sampling factors up to 4) is derived from stb_image v2.30's JPEG decoder: the Huffman table build and
+// fast-AC table (stb_image.h:2003-2073), the bit reader and block decoders (:2075-2413, incl. the
+// progressive refinement loop), the zig-zag table (:2194), the resampler loop and the blinn_8x8 rounding
+// (:3859) follow stb's code, so that the texels are the same bits (tests/test_image_load.py compares
+// against stb_image itself, compiled from the reference tree into oracle/_ref).  Numerical choices kept:
 //   - inverse DCT: the islow integer flow graph (jidctint), constants rounded to 12 fractional bits,
 //     columns first with +2^9 >> 10, rows with +2^16 + 128*2^17 >> 17, clamped to 0..255, in the lane
 //     widths of stb's SSE2 version (what the reference's x86-64 host runs);
@@ -20,6 +21,23 @@
 //   - out-of-data and marker handling of the entropy decoder (zero bits after the data ends, a restart
 //     marker expected every restart interval, junk after the last scan skipped).
 // It returns false where stbi_loadf returns NULL (the reference's texture then has no pixels).
+//
+// Provenance and licence.  Parts of this file are DERIVED FROM stb_image v2.30 (Sean Barrett and contributors,
+// http://nothings.org/stb), the third-party header the reference vendors as include/stb_image.h, and keep its
+// structure where bit-exactness with stbi_loadf (corrupt and truncated files included) requires the same
+// control flow.  stb_image is available under the MIT licence or as public domain (its ALTERNATIVE A / B);
+// this derived code is used under ALTERNATIVE A, whose notice follows:
+//   Copyright (c) 2017 Sean Barrett
+//   Permission is hereby granted, free of charge, to any person obtaining a copy of this software and
+//   associated documentation files (the "Software"), to deal in the Software without restriction, including
+//   without limitation the rights to use, copy, modify, merge, publish, distribute, sublicense, and/or sell
+//   copies of the Software, and to permit persons to whom the Software is furnished to do so, subject to the
+//   following conditions: The above copyright notice and this permission notice shall be included in all
+//   copies or substantial portions of the Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY
+//   KIND, EXPRESS OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A
+//   PARTICULAR PURPOSE AND NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR
+//   ANY CLAIM, DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR OTHERWISE, ARISING FROM,
+//   OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
 #include <algorithm>
 #include <cstdint>
 #include <cstring>

@@ -16,6 +16,24 @@
 // failed load, RT_IMAGE_MISSING: no pixels, the texture renders magenta (:346-347).  One deliberate
 // difference: where stb "succeeds" with a zero-area image (a BMP or HDR header saying width 0), the
 // reference's texel lookup would index outside the buffer; such a file is RT_IMAGE_MISSING here.
+// The BMP helpers high_bit / bitcount / shiftsigned are stb's (:5370-5413) with the same tables.
+//
+// Provenance and licence.  Parts of this file are DERIVED FROM stb_image v2.30 (Sean Barrett and contributors,
+// http://nothings.org/stb), the third-party header the reference vendors as include/stb_image.h, and keep its
+// structure where bit-exactness with stbi_loadf (corrupt and truncated files included) requires the same
+// control flow.  stb_image is available under the MIT licence or as public domain (its ALTERNATIVE A / B);
+// this derived code is used under ALTERNATIVE A, whose notice follows:
+//   Copyright (c) 2017 Sean Barrett
+//   Permission is hereby granted, free of charge, to any person obtaining a copy of this software and
+//   associated documentation files (the "Software"), to deal in the Software without restriction, including
+//   without limitation the rights to use, copy, modify, merge, publish, distribute, sublicense, and/or sell
+//   copies of the Software, and to permit persons to whom the Software is furnished to do so, subject to the
+//   following conditions: The above copyright notice and this permission notice shall be included in all
+//   copies or substantial portions of the Software.  THE SOFTWARE IS PROVIDED "AS IS", WITHOUT WARRANTY OF ANY
+//   KIND, EXPRESS OR IMPLIED, INCLUDING BUT NOT LIMITED TO THE WARRANTIES OF MERCHANTABILITY, FITNESS FOR A
+//   PARTICULAR PURPOSE AND NONINFRINGEMENT. IN NO EVENT SHALL THE AUTHORS OR COPYRIGHT HOLDERS BE LIABLE FOR
+//   ANY CLAIM, DAMAGES OR OTHER LIABILITY, WHETHER IN AN ACTION OF CONTRACT, TORT OR OTHERWISE, ARISING FROM,
+//   OUT OF OR IN CONNECTION WITH THE SOFTWARE OR THE USE OR OTHER DEALINGS IN THE SOFTWARE.
 #include <algorithm>
 #include <array>
 #include <climits>

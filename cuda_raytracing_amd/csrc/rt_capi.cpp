@@ -76,6 +76,7 @@ constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per 
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
 constexpr int kMixLanes = 32;                   // mixed hot waves (verified mixed walk): costly pixels per wave
 constexpr uint32_t kRcLdsMaxLevels = 256;  // colour-stack levels kept in LDS at most (max_bounces is a u8)
+constexpr uint32_t kSpanWord = 48;          // work words 48..51: the render kernel's span (RenderArgs::span)
 
 // LDS bytes of one colour-stack level for a 256-thread block: 32-bit codes, or 16-bit in narrow kernels
 constexpr size_t rc_level_bytes(bool narrow) { return static_cast<size_t>(rt::kWavesPerBlock) * 64 * (narrow ? 2 : 4); }
@@ -141,6 +142,7 @@ float ray_bound(const rt::SceneImage &img, const rt_camera *cam, const rt_params
 struct rt_context {
   int device = 0;
   int cu_count = 0;
+  double wall_khz = 100000.0;   // s_memrealtime ticks per ms (hipDeviceAttributeWallClockRate, kHz)
   SceneImage img;
   // verified sphere traversal (RT_TRAV_ACCEL): SAH tree words appended to the device scene image
   rt::SphereAccel accel;
@@ -361,6 +363,10 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { rt_context_destroy(c); return RT_ERR_HIP; }
   c->cu_count = prop.multiProcessorCount;
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) c->wall_khz = khz;
+  }
   const std::vector<uint32_t> &J = rt::xorwow_jump_tables();
   bool ok = c->scene.ensure(dev_words.size() * 4) == hipSuccess &&
             hipMemcpy(c->scene.p, dev_words.data(), dev_words.size() * 4, hipMemcpyHostToDevice) == hipSuccess &&
@@ -398,6 +404,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->counted = (p->flags & RT_FLAG_COUNT) != 0;
   c->samples = static_cast<uint64_t>(n) * static_cast<uint64_t>(p->samples_per_pixel);
   c->used_fold = false;
+  if ((n == 0 || mb == 0) && hipMemsetAsync(c->work.p, 0, 256, s) != hipSuccess) return RT_ERR_HIP;   // no span
   if (n == 0) {   // same event order as a render: seed | schedule | render, ev[2] (render end) last
     for (int k : {0, 1, 3, 2})
       if (hipEventRecord(c->ev[k], s) != hipSuccess) return RT_ERR_HIP;
@@ -441,7 +448,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   uint32_t scene_lds_words = c->lds ? static_cast<uint32_t>(c->img.words.size()) : 0;
   // colour stack: 16-bit codes in run-time compiled kernels of scenes without noise and texels (and with
   // < 65536 colour records), 32-bit otherwise; the LDS-scene decision is made with the wide size
-  const bool narrow_ok = !c->img.has_noise && !c->img.needs_uv && c->img.rec_consts + rt::kRcConsts <= 65536u;
+  const bool narrow_ok = !c->img.has_noise && !c->img.needs_uv && c->img.rec_consts + rt::kRcConsts < 65536u;   // code 0xffff stays unused (RC_AUDIT sentinel)
   uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
   size_t rc_bytes = rc_levels * rc_level_bytes(false);
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
@@ -555,6 +562,13 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (trav == RT_TRAV_ACCEL && !c->lds && c->accel_lds_nodes > 0) {
     accel_lds_nodes = std::min<uint32_t>(c->accel_lds_nodes,
                                          static_cast<uint32_t>(c->accel.node_words.size() / rt::kAccelNodeWords));
+    // only what the block's LDS budget leaves after the colour-stack levels and the stacks (an explicit
+    // RT_RC_LDS_LEVELS may already take most of it): the staging shrinks, the launch never exceeds 160 KiB
+    const bool nw = jit_fn != nullptr && narrow_ok;
+    const size_t used = (nw ? ((rc_levels + 1) & ~1u) : rc_levels) * rc_level_bytes(nw) + stack_bytes + kLdsReserve;
+    const size_t node_bytes = static_cast<size_t>(rt::kAccelNodeWords) * 4;
+    const size_t room = used < kLdsPerCu ? (kLdsPerCu - used) / node_bytes : 0;
+    accel_lds_nodes = static_cast<uint32_t>(std::min<size_t>(accel_lds_nodes, room));
     scene_lds_words = accel_lds_nodes * rt::kAccelNodeWords;
   }
   const bool narrow = jit_fn != nullptr && narrow_ok;   // the offline kernels use 32-bit codes
@@ -602,7 +616,10 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;
   c->used_rc_levels = rc_levels;
   c->rc_audit_bytes = 0;
-  if (p->flags & RT_FLAG_RC_AUDIT) {   // every slot 0xff..: a written code never is (rt_layout.h kRc*)
+  // every slot 0xff..: a written code never is — narrow codes are record indices < 65535 (narrow_ok), wide
+  // record codes have the sign bit clear, greys are finite with the sign clear, and a texel code's offset is at
+  // most pixel_words - 3 < 0x7fffffff (rt_layout.h kRc*)
+  if (p->flags & RT_FLAG_RC_AUDIT) {
     c->rc_audit_bytes = static_cast<size_t>(mb) * threads * (narrow ? 2 : 4);
     c->rc_audit_narrow = narrow;
     if (hipMemsetAsync(c->rc.p, 0xff, c->rc_audit_bytes, s) != hipSuccess) return RT_ERR_HIP;
@@ -673,6 +690,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.prio_lanes = 64u;   // no sparse waves (the probe launch keeps these defaults)
   a.prio_mix = 0u;
   a.tail_prio = 0u;   // the probe launch keeps it off
+  a.span = nullptr;   // set for the render launch below (the probe launch keeps no span)
   const uint32_t n_tiles = a.n_ids / 64u;
   c->used_lpt = c->sched == 3 || (c->sched == 0 && p->samples_per_pixel >= kLptMinSpp);
   a.wave_trace = nullptr;
@@ -750,6 +768,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // Tail issue priority: on for the verified mixed walk (final_scene 800x800 spp 64: 638-649 -> 598-611 ms
   // per frame), within noise elsewhere (scene 0 -1 %, 10k +1 %; profiles/r03_ab_tail_prio.jsonl)
   a.tail_prio = (c->tail_prio == 1 || (c->tail_prio < 0 && c->used_traversal == RT_TRAV_MIXED)) ? 1u : 0u;
+  a.span = reinterpret_cast<unsigned long long *>(static_cast<uint32_t *>(c->work.p) + kSpanWord);   // zeroed above
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
@@ -821,6 +840,14 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->sched_ms = b;
   st->render_ms = d;
   st->samples = c->samples;
+  st->devices = 1;
+  {   // the render kernel's own span (RenderArgs::span): first wave start to last wave end
+    unsigned long long sp[2] = {0, 0};
+    if (hipMemcpy(sp, static_cast<uint32_t *>(c->work.p) + kSpanWord, sizeof sp, hipMemcpyDeviceToHost) != hipSuccess)
+      return RT_ERR_HIP;
+    const unsigned long long t0 = ~sp[0], t1 = sp[1];
+    st->render_kernel_ms = (sp[0] != 0 && t1 >= t0) ? static_cast<double>(t1 - t0) / c->wall_khz : 0.0;
+  }
   if (c->rc_audit_bytes) {   // RT_FLAG_RC_AUDIT: slots the render wrote
     std::vector<uint8_t> rb(c->rc_audit_bytes);
     if (hipMemcpy(rb.data(), c->rc.p, rb.size(), hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
@@ -930,7 +957,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
   const int variant = (img.words.size() <= rt::kLdsSceneMaxWords ? rt::kVarLds : 0) | (img.has_noise ? rt::kVarNoise : 0) |
                       (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img) |
                       (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
-                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts <= 65536u ? rt::kVarNarrow : 0);
+                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0);
   std::string src;
   if (traversal == RT_TRAV_STATIC) {
     uint32_t v = 0;

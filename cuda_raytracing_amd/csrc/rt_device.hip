@@ -163,7 +163,36 @@ __global__ __launch_bounds__(256) void tonemap_kernel(const float *__restrict__ 
   }
 }
 
+// Multi-device frames (rt_multi.cpp): the root's gathered buffer holds n shards of max_rows rows each (shard g =
+// rows g, g + n, ... of the frame, RCCL gather order); frame row k is shard k % n, row k / n.  One block row per
+// frame row; 4-byte words when rows are word-sized, bytes otherwise.
+__global__ __launch_bounds__(256) void unpermute_kernel(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst,
+                                                        uint32_t rows, uint32_t n, uint32_t max_rows, uint32_t row_bytes) {
+  for (uint32_t k = blockIdx.y; k < rows; k += gridDim.y) {
+    const uint8_t *s = src + (static_cast<size_t>(k % n) * max_rows + k / n) * row_bytes;
+    uint8_t *d = dst + static_cast<size_t>(k) * row_bytes;
+    if ((row_bytes & 3u) == 0) {
+      const uint32_t *s4 = reinterpret_cast<const uint32_t *>(s);
+      uint32_t *d4 = reinterpret_cast<uint32_t *>(d);
+      for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < row_bytes / 4; i += gridDim.x * 256) d4[i] = s4[i];
+    } else {
+      for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < row_bytes; i += gridDim.x * 256) d[i] = s[i];
+    }
+  }
+}
+
 }  // namespace
+
+hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t n, uint32_t max_rows,
+                            uint32_t row_bytes, hipStream_t s) {
+  if (rows == 0 || row_bytes == 0) return hipSuccess;
+  if (n == 0 || static_cast<uint64_t>(n) * max_rows < rows) return hipErrorInvalidValue;
+  const uint32_t per = (row_bytes & 3u) == 0 ? row_bytes / 4 : row_bytes;
+  const uint32_t bx = (per + 255) / 256 < 16 ? (per + 255) / 256 : 16;
+  hipLaunchKernelGGL(unpermute_kernel, dim3(bx, rows < 65535u ? rows : 65535u), dim3(256), 0, s,
+                     static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), rows, n, max_rows, row_bytes);
+  return hipGetLastError();
+}
 
 hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_t s) {
   if (n == 0) return hipSuccess;

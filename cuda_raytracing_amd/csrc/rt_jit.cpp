@@ -425,11 +425,30 @@ int accel_waves() {
   return 6;
 }
 
+// The default 6-wave request is measured on the plain 10k walk, whose 80-VGPR build spills ~17 VGPRs outside
+// the node loop (44 B per lane).  Variants that need far more registers (noise, image u,v, deep bounces:
+// 125-149 VGPRs) would spill inside their hot loops; a default-request build with more scratch than this is
+// replaced by the allocator's own build (+ the residency raise).  An explicit RT_ACCEL_WAVES is kept as built.
+constexpr int kAccelWavesScratchMax = 96;
+
 bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
-  const int w = accel_waves();
+  int w = accel_waves();
   if (!build_module(jit_accel_source(img, variant, w), "rt_accel", out, why)) return false;
+  if (w > 0 && !std::getenv("RT_ACCEL_WAVES")) {
+    int sc = 0;
+    render_vgprs(out->render, &sc);
+    if (std::getenv("RT_DEBUG"))
+      std::fprintf(stderr, "[rt] jit accel waves_per_eu(%d): scratch %d B per lane\n", w, sc);
+    if (sc < 0 || sc > kAccelWavesScratchMax) {
+      JitKernels k = *out;
+      if (!build_module(jit_accel_source(img, variant, 0), "rt_accel", &k, why)) return false;
+      k.ms += out->ms;
+      *out = k;
+      w = 0;
+    }
+  }
   if (w == 0) raise_residency([&](int n) { return jit_accel_source(img, variant, n); }, "rt_accel", out);
   return true;
 }

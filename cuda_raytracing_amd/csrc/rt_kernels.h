@@ -16,6 +16,9 @@ hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_
 // longest-first order of n tiles from probe costs (single block)
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s);
 hipError_t launch_render(const RenderArgs &a, int variant, uint32_t blocks, size_t lds_bytes, hipStream_t s);
+// multi-device frames: frame row k <- row k / n of shard k % n in src ([n][max_rows][row_bytes])
+hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t n, uint32_t max_rows,
+                            uint32_t row_bytes, hipStream_t s);
 // resident 256-thread blocks per CU for the chosen variant (occupancy query)
 int render_blocks_per_cu(int variant, size_t lds_bytes);
 

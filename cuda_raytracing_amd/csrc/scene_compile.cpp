@@ -324,12 +324,25 @@ int compile_scene(const void *scene_ptr, SceneImage *img) {
   // sphere's u,v only for these (get_sphere_uv's values are read by nothing else); RT_LAZY_UV=0 (A/B): all
   const char *lz = std::getenv("RT_LAZY_UV");
   const bool lazy_uv = !(lz && lz[0] == '0');
+  // a texture reads u,v if it is an image or a checker with such a child anywhere below it (texture_color
+  // follows the checker recursion down to the image, :366-384); depth-bounded like texture() (cycles were
+  // rejected there, so the recursion ends)
+  std::vector<int8_t> reads_uv(img->tex_count, -1);
+  auto tex_reads_uv = [&](auto &&self, uint32_t ti, int depth) -> bool {
+    if (ti >= img->tex_count || depth > 64) return true;   // conservative
+    if (reads_uv[ti] >= 0) return reads_uv[ti] != 0;
+    const uint32_t *t = &c.texs[static_cast<size_t>(ti) * kTexWords];
+    bool r = t[T_KIND] == T_IMAGE;
+    if (t[T_KIND] == T_CHECKER) r = self(self, t[T_EVEN], depth + 1) || self(self, t[T_ODD], depth + 1);
+    reads_uv[ti] = r ? 1 : 0;
+    return r;
+  };
   for (uint32_t i = 0; i < sc->hittable_count; ++i) {
     uint32_t *w = &W[static_cast<size_t>(i) * kNodeWords];
     if (w[W_KIND] != K_SPHERE) continue;
     const uint32_t *m = &c.mats[static_cast<size_t>(w[W_AUX]) * kMatWords];
     const bool textured = m[M_KIND] == MAT_LAMBERTIAN || m[M_KIND] == MAT_DIFFUSE_LIGHT;
-    w[W_SPHERE_UV] = !lazy_uv || (textured && c.texs[static_cast<size_t>(m[M_TEX]) * kTexWords + T_KIND] == T_IMAGE) ? 1u : 0u;
+    w[W_SPHERE_UV] = !lazy_uv || (textured && tex_reads_uv(tex_reads_uv, m[M_TEX], 0)) ? 1u : 0u;
   }
   img->off_mats = static_cast<uint32_t>(W.size());
   W.insert(W.end(), c.mats.begin(), c.mats.end());

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* status codes */
 #define RT_OK                 0
@@ -138,6 +138,13 @@ typedef struct rt_stats {
   int32_t mix_macros;      /* RT_TRAV_MIXED: transform-free subtrees with a SAH walk (0 otherwise) */
   uint32_t mix_fallbacks;  /* RT_TRAV_MIXED: macro walks of the last render handed back to the reference walk */
   int32_t pad_;
+  /* ABI 5 */
+  double render_kernel_ms; /* the render kernel alone: its first wave's start to its last wave's end on the device's
+                              wall clock (s_memrealtime), what a profiler reports as the kernel duration; render_ms
+                              is the stream-event window around the launch (>= this) */
+  double gather_ms;        /* rt_multi_render / rt_render_devices: RCCL gather of the shards + on-device un-permute */
+  int32_t devices;         /* devices that rendered the frame (1 for the single-device entry points) */
+  int32_t pad2_;
 } rt_stats;
 
 /* rt_stats.jit_source */
@@ -171,6 +178,33 @@ int rt_context_render_ppm(rt_context *ctx, const rt_camera *camera, const rt_par
 int rt_context_timing(rt_context *ctx, rt_stats *stats);
 void rt_context_destroy(rt_context *ctx);
 
+/* ---- one process, several devices (rows interleaved across the GPUs of a node, one RCCL gather) ----
+ * The frame rows of `params` (row_offset + k*row_stride, k < row_count) are dealt round-robin: row k goes to
+ * devices[k % n].  Each device renders its shard with its own rt_context on its own stream (no exchange while
+ * rendering: pixels are independent and the RNG subsequence is the global pixel index, so the image is the same
+ * bits for any n); then ONE grouped ncclGather (RCCL, rccl.h:745) collects every shard's rows — the P6 bytes
+ * (3 B/px) and, when out_rgb is requested, the linear floats (12 B/px) — on devices[0], an un-permute kernel
+ * restores row order there, and the frame is copied to the host.  RCCL is loaded on first use (dlopen of
+ * librccl.so.1, the library torch.distributed's "nccl" backend also binds); without it these return
+ * RT_ERR_UNSUPPORTED.  devices: distinct HIP device ordinals (ncclCommInitAll, rccl.h:236).
+ * out_rgb (host, row_count*width*3 floats) and out_ppm (host, row_count*width*3 bytes, the P6 payload
+ * of pixels_to_ppm): either may be NULL, not both.  stats (optional): timings are the maximum over the
+ * devices, samples the total, plus gather_ms and devices.
+ * rt_render_devices is the one-shot form (create, render, destroy): the multi-GPU drop-in for the device half
+ * of render() (raytracing.cu:1694-1771, called once from main.cu:130). */
+typedef struct rt_multi rt_multi;
+int rt_multi_create(const rt_scene *scene, const int *devices, int n_devices, rt_multi **out);
+int rt_multi_render(rt_multi *m, const rt_camera *camera, const rt_params *params, float *out_rgb, uint8_t *out_ppm,
+                    rt_stats *stats);
+void rt_multi_destroy(rt_multi *m);
+int rt_render_devices(const rt_scene *scene, const rt_camera *camera, const rt_params *params, const int *devices,
+                      int n_devices, float *out_rgb, uint8_t *out_ppm, rt_stats *stats);
+/* The row deal of rt_multi_render (no device needed; tests): for the k-th row of a row_count-row frame over
+ * n_devices devices, *device = k % n_devices and *local = k / n_devices, the row's index in that device's shard;
+ * *shard_rows = that device's row count, *max_rows = the longest shard (the gather's per-device stride). */
+int rt_multi_row_map(int32_t row_count, int32_t n_devices, int32_t k, int32_t *device, int32_t *local,
+                     int32_t *shard_rows, int32_t *max_rows);
+
 /* Device tonemap: the byte conversion of pixels_to_ppm (raytracing.cu:1391-1395,
  * 1419-1431) — sqrt gamma, clamp [0, 0.999], (u8)(256 x) — from a device framebuffer of `pixels`
  * RGB float triples to 3*pixels device bytes (P6 payload order), asynchronously on `stream`.
@@ -184,11 +218,13 @@ int rt_tonemap_device(const float *rgb_device, uint64_t pixels, uint8_t *out_dev
 int rt_static_source(const rt_scene *scene, uint32_t max_visits, char *buf, uint64_t cap, uint32_t *visits);
 int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *arch, char *log, uint64_t cap);
 /* The run-time (hipRTC) source of any traversal's kernels for `scene` as a render with max_bounces
- * would build it (traversal = RT_TRAV_STATIC, RT_TRAV_ACCEL or RT_TRAV_LANE; no device needed):
- * ISA / register / scratch inspection with hipcc (tools/isa_stats.sh). */
+ * would build it (traversal = RT_TRAV_STATIC, RT_TRAV_ACCEL, RT_TRAV_MIXED or RT_TRAV_LANE; no device
+ * needed): ISA / register / scratch inspection with hipcc (tools/isa_stats.sh). */
 int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap);
 /* Diagnostics for the verified mixed-world traversal (no device needed): info = {macro roots, dynamic
- * ones, primitives in their SAH trees, deepest SAH tree}; RT_ERR_UNSUPPORTED when no subtree qualifies. */
+ * ones, primitives in their SAH trees, deepest SAH tree}; RT_ERR_UNSUPPORTED when no subtree qualifies.
+ * The build reads the RT_MIX_* environment knobs (e.g. RT_MIX_DYN_MIN, the dynamic-macro primitive
+ * threshold) exactly as rt_context_create does, so the counts depend on them. */
 int rt_mixed_build(const rt_scene *scene, uint32_t info[4]);
 /* Diagnostics for the verified sphere traversal (no device needed): builds the SAH tree of an
  * all-sphere world.  info = {root node, depth, spheres, node words}; words (if non-null, cap words)

@@ -63,3 +63,42 @@ def test_weak_scaled_resolution():
     assert weak_scaled_resolution(1920, 1080, 4) == (3840, 2160)
     W, H = weak_scaled_resolution(1920, 1080, 8)
     assert abs(W * H / (1920 * 1080) - 8) < 0.01
+
+
+# ---- one process, N devices through the C-ABI (rt_multi_render / rt_render_devices, rt_multi.cpp) ----
+# The device code is exercised by tests/test_gpu_parity.py (N = 1 on the GPU box); here the row deal and the
+# gather + un-permute are checked on the CPU: the shards the library's row map assigns, rendered by the oracle,
+# padded to the longest shard and concatenated in device order (ncclGather's layout on the root), then put back
+# in frame order through the same map, must give the single-process frame bit for bit.
+@pytest.mark.parametrize("H,n", [(17, 1), (17, 2), (17, 3), (18, 8), (5, 8), (1, 4), (30, 7)])
+def test_multi_row_map_gather_unpermute(H, n):
+    import cuda_raytracing_amd as rt
+    W = 20
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    rc, full, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=2, bounces=5))
+    assert rc == 0
+    maps = [rt.multi_row_map(H, n, k) for k in range(H)]
+    max_rows = maps[0][3]
+    assert max_rows == len(range(0, H, n))
+    # the deal is a bijection onto (device, local row) with every shard's rows contiguous from 0
+    assert sorted((d, l) for d, l, _, _ in maps) == sorted((d, l) for d in range(n) for l in range(len(range(d, H, n))))
+    for d, l, rows_d, m in maps:
+        assert rows_d == len(range(d, H, n)) and m == max_rows and l < rows_d
+    gathered = np.zeros((n * max_rows, W, 3), np.float32)
+    for d in range(n):
+        off, stride, cnt = rt.shard_rows(H, d, n)
+        assert cnt == len([1 for dd, _, _, _ in maps if dd == d])
+        if cnt:
+            rc, shard, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=2, bounces=5, row_offset=off,
+                                                                         row_stride=stride, row_count=cnt))
+            gathered[d * max_rows:d * max_rows + cnt] = shard
+    frame = np.stack([gathered[d * max_rows + l] for d, l, _, _ in maps])
+    assert np.array_equal(bits(frame), bits(full))
+
+
+def test_multi_row_map_rejects_bad_geometry():
+    import cuda_raytracing_amd as rt
+    for args in ((5, 0, 0), (5, 2, 5), (5, 2, -1), (-1, 2, 0)):
+        with pytest.raises(rt.RenderError):
+            rt.multi_row_map(*args)

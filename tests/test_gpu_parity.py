@@ -889,6 +889,48 @@ def test_mixed_walk_final_scene_full_size_rows():
     assert np.array_equal(bits(full[0::stride]), bits(ref))
 
 
+def _checker_of_image_world():
+    """Spheres whose checker texture has an image child (texture_get_color follows the checker recursion down
+    to the image, raytracing.cu:366-384): their u,v must be computed although the material's own texture is a
+    checker.  The builder API makes checkers of two solids only, so the checker's even TextureRef is patched in
+    the arena bytes to point at the image texture."""
+    import struct
+    w = rt.World(capacity=512)
+    yy, xx = np.mgrid[0:23, 0:41].astype(np.float32)
+    img = w.image_pixels(np.stack([xx / 40.0, yy / 22.0, 0.3 + 0.4 * ((xx + 2 * yy) % 5 == 0)], axis=-1).astype(np.float32))
+    chk = w.checker(0.9, (0.9, 0.2, 0.1), (0.1, 0.8, 0.3))
+    g = np.random.default_rng(77)
+    w.sphere((0.0, -100.5, -2.0), 100.0, w.lambert((0.5, 0.5, 0.5)))
+    for _ in range(80):   # a transform-free subtree for the SAH walk
+        c = (float(g.uniform(-3, 3)), float(g.uniform(-0.3, 1.5)), float(g.uniform(-6, -1.5)))
+        w.sphere(c, float(g.uniform(0.1, 0.35)), chk if g.uniform() < 0.6 else w.metal((0.8, 0.7, 0.6), 0.2))
+    w.box((-0.5, -0.5, -3.0), (0.5, 0.5, -2.0), chk, xf=rt.RT_XF_YROTATE_TRANSLATE, angle=25.0, offset=(1.0, 0.0, 0.0))
+    b = w.blobs()
+    tex = bytearray(b["textures"])
+    chk_off = struct.unpack_from("<Q", bytes(chk.payload), 0)[0]
+    img_off = struct.unpack_from("<Q", bytes(img.payload), 0)[0]
+    assert struct.unpack_from("<I", tex, chk_off)[0] == 1 and struct.unpack_from("<I", tex, img_off)[0] == 2
+    struct.pack_into("<Q", tex, chk_off + 16, img_off)   # checker.even -> the image texture
+    s = rt.Settings()
+    _abi.host_lib().rt_settings_default(C.byref(s))
+    s.lookfrom, s.lookat, s.vfov = rt.vec3(0, 1.0, 1.0), rt.vec3(0, 0.2, -3), 70.0
+    return rt.BlobScene(b["hittables"], b["refs"], bytes(tex), b["root"]), s
+
+
+def test_checker_of_image_spheres_compute_uv_vs_oracle():
+    # ADVICE r3: the lazy sphere-u,v flag must see an image below a checker; every traversal incl. the mixed walk
+    bs, s = _checker_of_image_world()
+    sc = bs.scene()
+    cam, W, H = rt.camera_from_settings(s, 64, 36)
+    p = rt.make_params(s, W, H, spp=4, bounces=8)
+    rc, ref, _ = oracle_render(sc, cam, p)
+    assert rc == 0 and len(np.unique(ref.reshape(-1, 3), axis=0)) > 100
+    for force in (0, rt.RT_FLAG_FORCE_MIXED, rt.RT_FLAG_FORCE_LANE, rt.RT_FLAG_FORCE_STATIC):
+        p.flags = force
+        fb, st = gpu(sc, cam, p)
+        assert np.array_equal(bits(fb), bits(ref)), (force, st.traversal)
+
+
 def test_image_texture_over_2_23_words_vs_oracle():
     # a texel pool of more than 2^23 words (a 1700x1700 float RGB map, 8.67 M words): colour-stack texel codes
     # carry 31-bit word offsets, so such scenes render (they were RT_ERR_UNSUPPORTED with 23-bit codes)
@@ -910,3 +952,50 @@ def test_image_texture_over_2_23_words_vs_oracle():
     assert rc == 0 and len(np.unique(ref.reshape(-1, 3), axis=0)) > 50
     fb, st = gpu(w.scene(), cam, p)
     assert np.array_equal(bits(fb), bits(ref))
+
+
+# ---- one process, N devices through the C-ABI (rt_render_devices: row deal, RCCL gather, un-permute) ----
+def test_render_devices_one_gpu_vs_oracle():
+    # the whole multi-device path with N = 1 (the GPU box has one device): RCCL communicator, the shard's render
+    # with PPM bytes, the grouped ncclGather of bytes and floats to the root, the un-permute kernel, the copy back
+    n_dev = C.c_int()
+    _abi.hip_lib().rt_device_count(C.byref(n_dev))
+    devices = list(range(min(n_dev.value, 8)))
+    for idx, W, H, spp, b in ((0, 96, 54, 8, 16), (20, 64, 36, 2, 16)):
+        w, s = rt.build_scene(idx)
+        cam, W, H = rt.camera_from_settings(s, W, H)
+        p = rt.make_params(s, W, H, spp=spp, bounces=b)
+        rc, ref, _ = oracle_render(w.scene(), cam, p)
+        assert rc == 0
+        f, u8, st = rt.render_devices(w.scene(), cam, p, devices, with_stats=True)
+        assert st.devices == len(devices) and st.samples == W * H * spp and st.render_kernel_ms > 0
+        assert np.array_equal(bits(f), bits(ref)) and np.array_equal(u8, rt.tonemap(ref))
+        # a row subset of the frame (strided rows, as one rank's shard of a larger job) through the same path
+        ps = rt.make_params(s, W, H, spp=spp, bounces=b, row_offset=1, row_stride=3)
+        rc, refs, _ = oracle_render(w.scene(), cam, ps)
+        f2, u2 = rt.render_devices(w.scene(), cam, ps, devices)
+        assert np.array_equal(bits(f2), bits(refs)) and np.array_equal(u2, rt.tonemap(refs))
+        # bytes only
+        none, u3 = rt.render_devices(w.scene(), cam, p, devices, rgb=False)
+        assert none is None and np.array_equal(u3, rt.tonemap(ref))
+
+
+def test_render_devices_rejects_bad_arguments():
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 16, 9)
+    p = rt.make_params(s, W, H, spp=1, bounces=4)
+    for devs in ([0, 0], [-1], [1 << 20]):
+        with pytest.raises(rt.RenderError) as e:
+            rt.render_devices(w.scene(), cam, p, devs)
+        assert e.value.code == _abi.RT_ERR_INVALID_ARG
+    with pytest.raises(rt.RenderError):
+        rt.render_devices(w.scene(), cam, p, [0], rgb=False, ppm=False)
+
+
+def test_kernel_span_within_event_window():
+    # rt_stats.render_kernel_ms (first wave start .. last wave end, s_memrealtime) is the kernel alone: positive and
+    # never above the stream-event window around the launch
+    w, s = rt.build_scene(0)
+    cam, W, H = rt.camera_from_settings(s, 320, 180)
+    fb, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=16, bounces=8))
+    assert 0 < st.render_kernel_ms <= st.render_ms * 1.001 + 0.01, (st.render_kernel_ms, st.render_ms)
