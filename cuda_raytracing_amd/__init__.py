@@ -352,6 +352,19 @@ def accel_build(scene: Scene):
     return {"root": info[0], "depth": info[1], "spheres": info[2]}, buf[:nw], buf[nw:]
 
 
+def accel_build_wide(scene: Scene):
+    """4-wide form of the verified walk's tree (no device needed): (info dict, node words as uint32), or None."""
+    L = _abi.hip_lib()
+    info = (C.c_uint32 * 4)()
+    rc = L.rt_accel_build_wide(C.byref(scene), None, 0, info)
+    if rc == _abi.RT_ERR_UNSUPPORTED:
+        return None
+    _check(rc, "rt_accel_build_wide")
+    buf = np.zeros(info[3], np.uint32)
+    _check(L.rt_accel_build_wide(C.byref(scene), buf.ctypes.data_as(C.c_void_p), len(buf), info), "rt_accel_build_wide")
+    return {"nodes": info[0], "depth": info[1], "stack": info[2]}, buf
+
+
 def mixed_build(scene: Scene):
     """Macro roots of the verified mixed-world traversal (no device needed): dict, or None when no
     transform-free subtree qualifies."""

@@ -12,7 +12,8 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 LIB_DIR = PKG_DIR / "lib"
-HIP_LIB = LIB_DIR / "librt_hip.so"
+# RT_HIP_LIB: another build of the render library (same-box A/B of two trees, tools/gpu_ab_env.sh); default in-tree
+HIP_LIB = Path(os.environ["RT_HIP_LIB"]) if os.environ.get("RT_HIP_LIB") else LIB_DIR / "librt_hip.so"
 HOST_LIB = LIB_DIR / "librt_host.so"
 ORACLE_LIB = REPO_DIR / "oracle" / "_build" / "liboracle_rt.so"
 
@@ -177,7 +178,7 @@ HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_contex
                "rt_context_destroy", "rt_status_string", "rt_device_count", "rt_abi_version",
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
                "rt_seed_states", "rt_kernel_source", "rt_mixed_build", "rt_multi_create", "rt_multi_render",
-               "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map"]
+               "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map", "rt_accel_build_wide", "rt_rng_row_bases"]
 
 
 def _bind_single_hip_runtime():
@@ -204,6 +205,11 @@ def hip_lib():
         _bind_single_hip_runtime()
         L = C.CDLL(str(HIP_LIB))
         P = C.c_void_p
+
+        # (entry points added in ABI 5 are bound when present: RT_HIP_LIB may name an older build for an A/B)
+        def opt(name, restype, *argtypes):
+            if hasattr(L, name):
+                _sig(getattr(L, name), restype, *argtypes)
         _sig(L.rt_render, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), P,
              C.POINTER(Stats))
         _sig(L.rt_context_create, C.c_int, C.POINTER(Scene), C.c_int, C.POINTER(C.c_void_p))
@@ -222,15 +228,17 @@ def hip_lib():
         _sig(L.rt_tonemap_device, C.c_int, P, C.c_uint64, P, P)
         _sig(L.rt_accel_build, C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
         _sig(L.rt_mixed_build, C.c_int, C.POINTER(Scene), C.POINTER(C.c_uint32))
+        opt("rt_accel_build_wide", C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
+        opt("rt_rng_row_bases", C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_seed_states, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_kernel_source, C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.c_char_p, C.c_uint64)
-        _sig(L.rt_multi_create, C.c_int, C.POINTER(Scene), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p))
-        _sig(L.rt_multi_render, C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P, C.POINTER(Stats))
-        _sig(L.rt_multi_destroy, None, P)
-        _sig(L.rt_render_devices, C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), C.POINTER(C.c_int),
-             C.c_int, P, P, C.POINTER(Stats))
+        opt("rt_multi_create", C.c_int, C.POINTER(Scene), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p))
+        opt("rt_multi_render", C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P, C.POINTER(Stats))
+        opt("rt_multi_destroy", None, P)
+        opt("rt_render_devices", C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), C.POINTER(C.c_int),
+            C.c_int, P, P, C.POINTER(Stats))
         i32p = C.POINTER(C.c_int32)
-        _sig(L.rt_multi_row_map, C.c_int, C.c_int32, C.c_int32, C.c_int32, i32p, i32p, i32p, i32p)
+        opt("rt_multi_row_map", C.c_int, C.c_int32, C.c_int32, C.c_int32, i32p, i32p, i32p, i32p)
         _hip = L
     return _hip
 

@@ -191,5 +191,57 @@ struct Builder {
   }
 };
 
+// 4-wide nodes from a (breadth-first) BVH2 in the kAccelNodeWords layout: each wide node holds the subtrees
+// reached from a BVH2 node by opening, twice, the internal child with the largest padded box surface.  The
+// child boxes are the BVH2's own padded boxes (the culling of every sphere is unchanged: a wide child box is
+// exactly the box the BVH2 walk would test at that subtree).  Wide nodes are numbered breadth-first from the
+// root (node 0).  depth_out: levels of the wide tree.
+inline std::vector<uint32_t> collapse_wide(const std::vector<uint32_t> &nodes, uint32_t root, uint32_t *depth_out) {
+  auto area = [](const uint32_t *b) {
+    const double dx = fl(b[1]) - fl(b[0]), dy = fl(b[3]) - fl(b[2]), dz = fl(b[5]) - fl(b[4]);
+    return (dx >= 0 && dy >= 0 && dz >= 0) ? 2.0 * (dx * dy + dy * dz + dz * dx) : 0.0;
+  };
+  struct Kid { const uint32_t *box; uint32_t ref; };
+  std::vector<uint32_t> out;
+  std::vector<uint32_t> queue{root}, level{1};
+  uint32_t depth = 0;
+  for (size_t qi = 0; qi < queue.size(); ++qi) {
+    const uint32_t *w = &nodes[static_cast<size_t>(queue[qi]) * kAccelNodeWords];
+    depth = std::max(depth, level[qi]);
+    std::vector<Kid> kids{{w, w[12]}, {w + 6, w[13]}};
+    while (kids.size() < 4) {
+      int open = -1;
+      double best = -1.0;
+      for (size_t i = 0; i < kids.size(); ++i)
+        if (!(kids[i].ref & kAccelLeaf) && area(kids[i].box) > best) { best = area(kids[i].box); open = static_cast<int>(i); }
+      if (open < 0) break;
+      const uint32_t *cw = &nodes[static_cast<size_t>(kids[open].ref) * kAccelNodeWords];
+      kids.erase(kids.begin() + open);
+      kids.push_back({cw, cw[12]});
+      kids.push_back({cw + 6, cw[13]});
+    }
+    const size_t base = out.size();
+    out.resize(base + kAccel4NodeWords, 0);
+    uint32_t *o = &out[base];
+    for (int c = 0; c < 4; ++c) {
+      for (int k = 0; k < 6; ++k)
+        o[4 * k + c] = (k & 1) ? fb(-std::numeric_limits<float>::infinity()) : fb(std::numeric_limits<float>::infinity());
+      o[kAccel4Ref + c] = 0;
+    }
+    for (size_t c = 0; c < kids.size(); ++c) {
+      for (int k = 0; k < 6; ++k) o[4 * k + c] = kids[c].box[k];
+      if (kids[c].ref & kAccelLeaf) {
+        o[kAccel4Ref + c] = kids[c].ref;
+      } else {
+        o[kAccel4Ref + c] = static_cast<uint32_t>(queue.size());   // breadth-first numbering
+        queue.push_back(kids[c].ref);
+        level.push_back(level[qi] + 1);
+      }
+    }
+  }
+  *depth_out = depth;
+  return out;
+}
+
 }  // namespace accel
 }  // namespace rt

@@ -84,6 +84,29 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return r;
 }
 
+// x <- P x through the nibble table of P (kRngNibTableWords at byte tb of the buffer rs): 40 lookups of 5 words,
+// XOR-summed.  Raw buffer loads (scalar descriptor + one 32-bit offset VGPR per gather) in twenty groups of two
+// (a rolled loop: one group's gathers in flight together, without the registers of a fully unrolled product;
+// this runs once per tile pickup, not per sample)
+__device__ __forceinline__ void rng_jump_nib(__amdgpu_buffer_rsrc_t rs, uint32_t tb, uint32_t &x0, uint32_t &x1,
+                                             uint32_t &x2, uint32_t &x3, uint32_t &x4) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  uint32_t r0 = 0, r1 = 0, r2 = 0, r3 = 0, r4 = 0;
+#pragma unroll 1
+  for (uint32_t g = 0; g < 20; ++g) {
+    const uint32_t w = g >> 2;
+    const uint32_t xw = (w == 0 ? x0 : (w == 1 ? x1 : (w == 2 ? x2 : (w == 3 ? x3 : x4)))) >> ((g & 3u) * 8u);
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+      const uint32_t e = (g * 2 + q) * 16 + ((xw >> (4 * q)) & 15u);
+      const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, tb + e * 16u, 0, 0);
+      r0 ^= a.x; r1 ^= a.y; r2 ^= a.z; r3 ^= a.w;
+      r4 ^= __builtin_amdgcn_raw_buffer_load_b32(rs, tb + 40u * 16u * 16u + e * 4u, 0, 0);
+    }
+  }
+  x0 = r0; x1 = r1; x2 = r2; x3 = r3; x4 = r4;
+}
+
 struct Rng {
   uint32_t d, x0, x1, x2, x3, x4;
   __device__ __forceinline__ uint32_t next() {
@@ -539,8 +562,9 @@ __device__ __forceinline__ void planar_hit(Trav &T, const Ray &r, Hit &h, bool t
 
 // sphere branch (:1093-1123) + sphere_get_uv (:583-590, image textures only)
 template <bool UV>
-__device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
+__device__ __forceinline__ bool sphere_hit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float rad2,
                                            float inv_rad, bool in_xf, bool need_uv = true) {
+  bool acc = false;
   f3 center = line_at(c0, r.time, mv);
   f3 oc = sub(center, r.o);
   float a = dot(r.d, r.d);
@@ -568,8 +592,10 @@ __device__ __forceinline__ void sphere_hit(Trav &T, const Ray &r, Hit &h, uint32
       T.tmax = h.t;
       T.result = true;
       if (in_xf) T.was_last = 1;
+      acc = true;
     }
   }
+  return acc;
 }
 
 // sphere with a constant centre (scene_codegen.cpp folds c + mv*time when mv = +-0)
@@ -662,7 +688,10 @@ __device__ __forceinline__ void rotate_exit_dir(Trav &T, Ray &r, Hit &h, float s
 // ALL: load the whole 80-B record at once (one memory latency per step instead of the kind word, then
 // the rest: the main per-lane walk of large scenes); the verified walk's rare fallback keeps the
 // two-step load, which needs fewer registers
-template <bool LDS, bool COUNT, bool UV, uint32_t KM = 0x7fu, bool ALL = true>
+// TRACK: an accepted sphere also leaves its record index in T.abest (| kBestRecord): the verified sphere walk's
+// fallback, whose hit record is rebuilt at shading time (AccelTraceK::materialize)
+constexpr uint32_t kBestRecord = 0x80000000u;
+template <bool LDS, bool COUNT, bool UV, uint32_t KM = 0x7fu, bool ALL = true, bool TRACK = false>
 __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hit &h, uint16_t *stk, Visits &vc) {
   int sp = T.sp - 1;
   const uint32_t idx = stk[sp * 64];
@@ -687,8 +716,9 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
                mk(asf(w3.x), asf(w3.y), asf(w3.z)), mk(asf(w3.w), asf(w4.x), asf(w4.y)), in_xf);
   } else if ((KM & (1u << K_SPHERE)) && kind == K_SPHERE) {
     if (!ALL) { w1 = S.w4(nb + 4); w2 = S.w4(nb + 8); }
-    sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
-                   asf(w2.y), asf(w2.z), in_xf);
+    if (sphere_hit<UV>(T, r, h, w0.y, mk(asf(w0.z), asf(w0.w), asf(w1.x)), mk(asf(w1.y), asf(w1.z), asf(w1.w)),
+                       asf(w2.y), asf(w2.z), in_xf) && TRACK)
+      T.abest = idx | kBestRecord;
   } else if ((KM & (1u << K_TRANSLATE)) && kind == K_TRANSLATE) {
     if (!ALL) w1 = S.w4(nb + 4);
     const f3 off = mk(asf(w0.z), asf(w0.w), asf(w1.x));
@@ -725,7 +755,7 @@ __device__ __forceinline__ void trav_step(const Mem<LDS> &S, Trav &T, Ray &r, Hi
 // PAUSE: the walk may stop at the end of a round with its state kept in T and the LDS stack (as in
 // AccelTraceK: the round's walk ends once at most A.defer_trace lanes, <= 1/4 of the starters, are
 // still walking after A.trace_min_iters steps); the walk resumes next round with shading skipped.
-template <uint32_t KM, bool PAUSE = false, bool ALL = true>
+template <uint32_t KM, bool PAUSE = false, bool ALL = true, bool TRACK = false>
 struct LaneTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t, uint32_t,
@@ -737,7 +767,7 @@ struct LaneTraceK {
       T.sp = 1;
     }
     if (!PAUSE) {
-      while (T.sp > 0) trav_step<LDS, COUNT, UV, KM, ALL>(S, T, r, h, stk, vc);
+      while (T.sp > 0) trav_step<LDS, COUNT, UV, KM, ALL, TRACK>(S, T, r, h, stk, vc);
       return;
     }
     const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(true)));
@@ -812,7 +842,7 @@ __device__ __forceinline__ bool accel_box(const Trav &T, const SlabRay &R, float
 // after the last step (sphere_commit, from the closest sphere's index) instead of at every acceptance:
 // the same operations on the same values, outside the loop.
 template <bool UV>
-__device__ __forceinline__ void sphere_commit(Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float inv_rad,
+__device__ __forceinline__ void sphere_commit(const Trav &T, const Ray &r, Hit &h, uint32_t mat, f3 c0, f3 mv, float inv_rad,
                                               bool need_uv = true) {
   const f3 center = line_at(c0, r.time, mv);
   h.t = T.tmax;
@@ -870,7 +900,22 @@ __device__ __forceinline__ bool sphere_hit_tie(Trav &T, const Ray &r, Hit &h, ui
   return true;
 }
 
-template <uint32_t KM>
+// sort network on 4 keys (ascending)
+__device__ __forceinline__ void sort4(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d) {
+  uint32_t t;
+  t = min(a, b); b = max(a, b); a = t;
+  t = min(c, d); d = max(c, d); c = t;
+  t = min(a, c); c = max(a, c); a = t;
+  t = min(b, d); d = max(b, d); b = t;
+  t = min(b, c); c = max(b, c); b = t;
+}
+
+// W4: the 4-wide form of the tree (rt_layout.h kAccel4*, accel::collapse_wide) — the same padded child boxes
+// and leaves, about half the node steps (each testing four boxes): the nearest hit inner child is visited next,
+// the others pushed far to near, the spheres of every hit leaf child tested in the step (one per-lane loop).
+// Every sphere is culled by exactly the box the 2-wide walk would test for it, so the record, the tie flag and
+// the reach proof are those of the 2-wide walk.
+template <uint32_t KM, bool W4 = false>
 struct AccelTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t lanes,
@@ -894,7 +939,7 @@ struct AccelTraceK {
     const Hit hsave = h;
     bool tie = resume && (T.anode >> 31) != 0;
     uint32_t best = resume ? T.abest : 0u;
-    const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
+    const uint4 *N = reinterpret_cast<const uint4 *>(A.scene + (W4 ? A.accel_wide : A.accel_nodes));
     const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.accel_prims);
     bool walking = nice;
     if (nice) {
@@ -904,7 +949,7 @@ struct AccelTraceK {
       const SlabRay sr = slab_ray(T, oinv, pinv);
       const float sa2 = 2.0f * dot(r.d, r.d);   // sphere_hit_tie's per-ray terms
       const float sra2 = rcp_ref(sa2);
-      uint32_t node = resume ? (T.anode & 0xffffu) : A.accel_root;
+      uint32_t node = resume ? (T.anode & 0xffffu) : (W4 ? 0u : A.accel_root);
       int sp = resume ? static_cast<int>((T.anode >> 16) & 0x7fffu) : 0;
       // Wave-uniform loop, one node per walking lane per step.  Rays differ wildly in length (the
       // horizon of a sphere field vs a close hit), so instead of every lane waiting for the longest
@@ -924,7 +969,80 @@ struct AccelTraceK {
         }
       };
       for (uint32_t it = 1;; ++it) {
-        if (walking) {
+        if (W4 && walking) {
+          // planes x0 x1 y0 y1 z0 z1 of the four children and their refs, 16 B each, from one base address with
+          // immediate offsets (LDS for the staged top of the tree, else global: two explicit loads, not a flat one)
+          // (address-space-typed pointers: merged into one generic pointer, the two paths become flat loads)
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          u32x4 v[7];
+          if (node < A.accel_lds_nodes) {
+            const __attribute__((address_space(3))) u32x4 *L =
+                (const __attribute__((address_space(3))) u32x4 *)(static_cast<uintptr_t>(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(g_lds)))) + node * 8;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) v[k] = L[k];
+          } else {
+            const __attribute__((address_space(1))) u32x4 *G =
+                (const __attribute__((address_space(1))) u32x4 *)(reinterpret_cast<uintptr_t>(N)) + node * 8;
+#pragma unroll
+            for (int k = 0; k < 7; ++k) v[k] = G[k];
+          }
+          const uint4 X0 = make_uint4(v[0].x, v[0].y, v[0].z, v[0].w), X1 = make_uint4(v[1].x, v[1].y, v[1].z, v[1].w);
+          const uint4 Y0 = make_uint4(v[2].x, v[2].y, v[2].z, v[2].w), Y1 = make_uint4(v[3].x, v[3].y, v[3].z, v[3].w);
+          const uint4 Z0 = make_uint4(v[4].x, v[4].y, v[4].z, v[4].w), Z1 = make_uint4(v[5].x, v[5].y, v[5].z, v[5].w);
+          const uint4 R4 = make_uint4(v[6].x, v[6].y, v[6].z, v[6].w);
+          // near / far plane per axis by the ray's octant (the near plane is the max one when 1/d < 0)
+          const uint4 XN = sr.nx ? X1 : X0, XF = sr.nx ? X0 : X1, YN = sr.ny ? Y1 : Y0, YF = sr.ny ? Y0 : Y1;
+          const uint4 ZN = sr.nz ? Z1 : Z0, ZF = sr.nz ? Z0 : Z1;
+          if (COUNT) vc.xn += 2;   // four boxes: two 2-wide steps' worth (the op model's per-step weight)
+          const uint32_t xn[4] = {XN.x, XN.y, XN.z, XN.w}, xf[4] = {XF.x, XF.y, XF.z, XF.w};
+          const uint32_t yn[4] = {YN.x, YN.y, YN.z, YN.w}, yf[4] = {YF.x, YF.y, YF.z, YF.w};
+          const uint32_t zn[4] = {ZN.x, ZN.y, ZN.z, ZN.w}, zf[4] = {ZF.x, ZF.y, ZF.z, ZF.w};
+          const uint32_t rr[4] = {R4.x, R4.y, R4.z, R4.w};
+          uint32_t key[4], cnt[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            // accel_box with the planes already in near / far order
+            const float tnx = __builtin_fmaf(asf(xn[c]), T.inv.x, sr.on.x), tfx = __builtin_fmaf(asf(xf[c]), T.inv.x, sr.of.x);
+            const float tny = __builtin_fmaf(asf(yn[c]), T.inv.y, sr.on.y), tfy = __builtin_fmaf(asf(yf[c]), T.inv.y, sr.of.y);
+            const float tnz = __builtin_fmaf(asf(zn[c]), T.inv.z, sr.on.z), tfz = __builtin_fmaf(asf(zf[c]), T.inv.z, sr.of.z);
+            const float t0 = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, kTmin)), t1 = fminf(fminf(tfx, tfy), fminf(tfz, T.tmax));
+            const bool hit = !(t1 < t0);
+            const bool leaf = (rr[c] & kAccelLeaf) != 0;
+            // inner children: sortable key = the entry t's high bits (t >= tmin > 0: monotone as an integer)
+            // with the node index in the low 16 bits (only the visit order depends on the truncation)
+            key[c] = (hit && !leaf) ? ((__float_as_uint(t0) & 0xffff0000u) | rr[c]) : 0xffffffffu;
+            cnt[c] = (hit && leaf) ? ((rr[c] >> 24) & 0x7fu) + 1u : 0u;
+          }
+          // the hit leaves' spheres, in one per-lane loop below: sphere k of the concatenated ranges
+          const uint32_t p1 = cnt[0], p2 = p1 + cnt[1], p3 = p2 + cnt[2], tot = p3 + cnt[3];
+          const uint32_t b0 = rr[0] & 0xffffffu, b1 = (rr[1] & 0xffffffu) - p1, b2 = (rr[2] & 0xffffffu) - p2,
+                         b3 = (rr[3] & 0xffffffu) - p3;
+          // next node first (the order does not depend on the leaves): the nearest hit inner child, the others
+          // pushed far to near (the nearest of them on top); none: pop
+          sort4(key[0], key[1], key[2], key[3]);
+          if (key[0] != 0xffffffffu) {
+            const int n_in = 1 + (key[1] != 0xffffffffu) + (key[2] != 0xffffffffu) + (key[3] != 0xffffffffu);
+            if (n_in >= 4) stk[(sp + n_in - 4) * 64] = static_cast<uint16_t>(key[3]);
+            if (n_in >= 3) stk[(sp + n_in - 3) * 64] = static_cast<uint16_t>(key[2]);
+            if (n_in >= 2) stk[(sp + n_in - 2) * 64] = static_cast<uint16_t>(key[1]);
+            sp += n_in - 1;
+            node = key[0] & 0xffffu;
+          } else if (sp == 0) {
+            walking = false;
+          } else {
+            --sp;
+            node = stk[sp * 64];
+          }
+          for (uint32_t k = 0; k < tot; ++k) {
+            const uint32_t pr = (k < p1 ? b0 : (k < p2 ? b1 : (k < p3 ? b2 : b3))) + k;
+            if (COUNT) vc.xp++;
+            const uint4 p0 = P[pr * 4], pw1 = P[pr * 4 + 1], pw2 = P[pr * 4 + 2];
+            if (sphere_hit_tie<UV, true, false>(T, r, h, pw2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)),
+                                                mk(asf(p0.w), asf(pw1.x), asf(pw1.y)), asf(pw1.z), asf(pw1.w), sa2, sra2, tie))
+              best = pr;
+          }
+        }
+        if (!W4 && walking) {
         load_node(node);
         if (COUNT) vc.xn++;
         float n0, n1;
@@ -979,30 +1097,68 @@ struct AccelTraceK {
       nice = false;
     }
     bool need_ref = !nice || tie;
+    T.abest = best;   // the record is rebuilt from it at shading time (materialize)
     if (nice && T.result) {
-      const uint4 p0 = P[best * 4], p1 = P[best * 4 + 1], p2 = P[best * 4 + 2];
-      sphere_commit<UV>(T, r, h, p2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)), mk(asf(p0.w), asf(p1.x), asf(p1.y)), asf(p1.w));
-      // (2): the hit point inside P's deepest reference BVH ancestor box with a margin of 2^-19 of
-      // the magnitudes the slab test and the hit point round (|o|, |p|, |t d| per axis): the
-      // reference's slab values err by <= 3u |x - o| and p by <= 2u (|o| + |t d|), u = 2^-24
+      // (2): the hit point (sphere_commit's: line_at(o, t, d)) inside P's deepest reference BVH ancestor box with
+      // a margin of 2^-19 of the magnitudes the slab test and the hit point round (|o|, |p|, |t d| per axis):
+      // the reference's slab values err by <= 3u |x - o| and p by <= 2u (|o| + |t d|), u = 2^-24
+      const float t = T.tmax;
+      const f3 hp = line_at(r.o, t, r.d);
       const uint4 b0 = P[best * 4 + 2], b1 = P[best * 4 + 3];
       const float bx0 = asf(b0.z), bx1 = asf(b0.w), by0 = asf(b1.x), by1 = asf(b1.y), bz0 = asf(b1.z), bz1 = asf(b1.w);
       const float m = 1.9073486328125e-06f;   // 2^-19
-      const float dx = m * (fabsf(r.o.x) + fabsf(h.p.x) + fabsf(h.t * r.d.x)) + 1.0e-30f;
-      const float dy = m * (fabsf(r.o.y) + fabsf(h.p.y) + fabsf(h.t * r.d.y)) + 1.0e-30f;
-      const float dz = m * (fabsf(r.o.z) + fabsf(h.p.z) + fabsf(h.t * r.d.z)) + 1.0e-30f;
-      const bool inside = (h.p.x - bx0 >= dx) & (bx1 - h.p.x >= dx) & (h.p.y - by0 >= dy) & (by1 - h.p.y >= dy) &
-                          (h.p.z - bz0 >= dz) & (bz1 - h.p.z >= dz);
+      const float dx = m * (fabsf(r.o.x) + fabsf(hp.x) + fabsf(t * r.d.x)) + 1.0e-30f;
+      const float dy = m * (fabsf(r.o.y) + fabsf(hp.y) + fabsf(t * r.d.y)) + 1.0e-30f;
+      const float dz = m * (fabsf(r.o.z) + fabsf(hp.z) + fabsf(t * r.d.z)) + 1.0e-30f;
+      const bool inside = (hp.x - bx0 >= dx) & (bx1 - hp.x >= dx) & (hp.y - by0 >= dy) & (by1 - hp.y >= dy) &
+                          (hp.z - bz0 >= dz) & (bz1 - hp.z >= dz);
       need_ref |= !inside;
     }
     const uint64_t fb = __ballot(need_ref);
-    if (fb != 0) {   // rare: the reference walk for those lanes
+    if (fb != 0) {   // rare: the reference walk for those lanes (it leaves the accepted record's index in T.abest)
       asm volatile("" ::: "memory");
       if (!COUNT && lane == static_cast<uint32_t>(__builtin_ctzll(fb))) atomicAdd(A.accel_fallbacks, static_cast<uint32_t>(__popcll(fb)));
-      LaneTraceK<KM, false, false>::template run<LDS, COUNT, UV>(S, A, need_ref, lanes, lane, stk, T, r, h, vc);
+      LaneTraceK<KM, false, false, true>::template run<LDS, COUNT, UV>(S, A, need_ref, lanes, lane, stk, T, r, h, vc);
     }
   }
+
+  // The hit record, rebuilt at shading time from (T.abest, T.tmax, the ray) for EVERY lane (values of lanes
+  // without a hit are never read): the record of a sphere hit is a function of the sphere, the root and the ray
+  // only (sphere_commit performs sphere_hit's record operations, :1093-1123), so the walk keeps two words per
+  // lane instead of the record, and no record is carried across the walk or across rounds (a lane resuming its
+  // rejection sampling rebuilds the same record from the same words).  T.abest: a SAH prim, or | kBestRecord a
+  // reference record (the fallback walk's hit).
+  static constexpr bool kLazyHit = true;
+  template <bool LDS, bool UV>
+  __device__ __forceinline__ static void materialize(const Mem<LDS> &S, const RenderArgs &A, const Trav &T, const Ray &r,
+                                                     Hit &h) {
+    const uint32_t b = T.abest;
+    uint4 w0, w1, w2;
+    uint32_t mat;
+    float inv_rad;
+    if (b & kBestRecord) {   // reference record: w1 material, w2..4 centre, w5..7 motion, w10 1/r
+      const uint32_t nb = (b & 0xffffu) * kNodeWords;
+      w0 = S.w4(nb); w1 = S.w4(nb + 4); w2 = S.w4(nb + 8);
+      mat = w0.y;
+      inv_rad = asf(w2.z);
+      w0 = make_uint4(w0.z, w0.w, w1.x, w1.y);   // centre x y z, motion x
+      w1 = make_uint4(w1.z, w1.w, 0u, 0u);       // motion y z
+    } else {                  // SAH prim: centre 0..2, motion 3..5, 1/r 7, material 8
+      const uint4 *P = reinterpret_cast<const uint4 *>(A.scene + A.accel_prims) + b * 4;
+      w0 = P[0]; w2 = P[1];
+      const uint4 w3 = P[2];
+      mat = w3.x;
+      inv_rad = asf(w2.w);
+      w1 = make_uint4(w2.x, w2.y, 0u, 0u);
+    }
+    sphere_commit<UV>(T, r, h, mat, mk(asf(w0.x), asf(w0.y), asf(w0.z)), mk(asf(w0.w), asf(w1.x), asf(w1.y)),
+                      inv_rad, T.result);
+  }
 };
+
+// Traces whose hit record is rebuilt at shading time (kLazyHit) — detected without <type_traits> (hipRTC)
+template <class TR> __device__ constexpr auto lazy_hit(int) -> decltype(TR::kLazyHit, bool()) { return TR::kLazyHit; }
+template <class TR> __device__ constexpr bool lazy_hit(long) { return false; }
 
 // ---------------------------------------------------------------------------------------------
 // traversal policy 5: verified traversal of mixed worlds (mixed_accel.cpp)
@@ -1577,10 +1733,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
     for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
     __syncthreads();
-  } else if (A.accel_lds_nodes) {   // the verified walk's top nodes (4 uint4 each)
-    const uint4 *src = reinterpret_cast<const uint4 *>(A.scene + A.accel_nodes);
+  } else if (A.accel_lds_nodes) {   // the verified walk's top nodes (4 uint4 each; 8 in the 4-wide tree)
+    const uint4 *src = reinterpret_cast<const uint4 *>(A.scene + (A.accel_wide ? A.accel_wide : A.accel_nodes));
     uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
-    for (uint32_t i = threadIdx.x; i < A.accel_lds_nodes * 4; i += kBlock) dst[i] = src[i];
+    const uint32_t n4 = A.accel_lds_nodes * (A.accel_wide ? 8u : 4u);
+    for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
     __syncthreads();
   }
   const uint32_t lane = __lane_id();
@@ -1639,6 +1796,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   uint32_t c_bounce = 0, c_shade = 0, c_perlin = 0, c_samples = 0;
 
   uint32_t chunk_pos = 0, chunk_end = 0;   // wave-uniform: ids of the wave's current tile
+  uint32_t chunk_base = 0;                 // wave-uniform: the first id of the chunk whose states are in the slot
+  // the wave's slot: a wave-uniform base (scalar registers; threadIdx.x >> 6 is not known to be uniform) and
+  // 32-bit per-lane offsets
+  char *const rng_slot = reinterpret_cast<char *>(A.rng_slot) +
+                         static_cast<size_t>(__builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave)) * kRngSlotWords * 4u;
   bool exhausted = false;
   bool prio_done = false;                  // wave-uniform: the split costliest tiles are all handed out
   uint32_t tiles_taken = 0, rounds = 0;
@@ -1651,14 +1813,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool lone = false;                                         // with at most 2 busy lanes (the frame's tail)
   const uint64_t t_start = TRACE ? __builtin_amdgcn_s_memrealtime() : 0;
 
-  f3 pp = mk(0, 0, 0);   // the pixel's viewport point (:1565-1567), computed once per pixel
   uint32_t pending = 0;   // 1: the lane's rejection sampling continues next round (A.max_tries)
   float random_test = 0.0f;
   const uint32_t try_cap = A.max_tries ? A.max_tries : 0xffffffffu;
-  auto pixel_point = [&]() {
+  // the pixel's viewport point (:1565-1567), recomputed per sample from pix (a few ops; three fewer registers
+  // carried across the trace)
+  auto pixel_point = [&]() -> f3 {
     const int32_t lr = pix / A.width, j = pix - lr * A.width;
     const int32_t i = A.row_offset + lr * A.row_stride;
-    pp = add(mk(A.p00[0], A.p00[1], A.p00[2]),
+    return add(mk(A.p00[0], A.p00[1], A.p00[2]),
              add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
                  scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
   };
@@ -1679,7 +1842,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     float xo = rng.uniform() - 0.5f;
     float yo = rng.uniform() - 0.5f;
-    ray.d = sub(pp, ray.o);
+    ray.d = sub(pixel_point(), ray.o);
     ray.d = add(ray.d, scale(xo, mk(A.du[0], A.du[1], A.du[2])));
     ray.d = add(ray.d, scale(yo, mk(A.dv[0], A.dv[1], A.dv[2])));
     ray.time = rng.uniform();
@@ -1748,6 +1911,37 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         tiles_taken++;
         chunk_pos = base;
         chunk_end = min(base + size, A.n_ids);
+        if (!probe) {
+          // RNG seeding of the chunk (init_gpu_data's curand_init, :1591-1606, subsequence = global pixel index
+          // i * W + j): lane l takes id base + l, starts from the state of its row (row base, subsequence i * W)
+          // and jumps over the column j by the binary powers P_k = J^(2^k) (bits >= 3 of j are the tile column,
+          // wave-uniform); the states wait in the wave's slot for the lanes that take those pixels
+          const uint32_t id = base + lane;
+          uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0, jcol = 0;
+          if (id < chunk_end) {
+            uint32_t tile = id >> 6;
+            const uint32_t kk = id & 63u;
+            if (A.tile_order) tile = A.tile_order[tile];
+            const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
+            const uint32_t lr = ty * 8 + (kk >> 3), j = tx * 8 + (kk & 7u);
+            if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
+              const uint4 rb = *reinterpret_cast<const uint4 *>(A.rng_rows + lr * 8);
+              x0 = rb.x; x1 = rb.y; x2 = rb.z; x3 = rb.w; x4 = A.rng_rows[lr * 8 + 4];
+              jcol = j;
+            }
+          }
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(A.rng_nib), 0,
+                                                                              0x7fffffff, 0x00020000);
+          for (uint32_t b = 0; __ballot((jcol >> b) != 0u) != 0; ++b)
+            if ((jcol >> b) & 1u) rng_jump_nib(rs, b * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
+          *reinterpret_cast<uint32_t *>(rng_slot + lane * 4u) = x0;
+          *reinterpret_cast<uint32_t *>(rng_slot + 256u + lane * 4u) = x1;
+          *reinterpret_cast<uint32_t *>(rng_slot + 512u + lane * 4u) = x2;
+          *reinterpret_cast<uint32_t *>(rng_slot + 768u + lane * 4u) = x3;
+          *reinterpret_cast<uint32_t *>(rng_slot + 1024u + lane * 4u) = x4;
+          __threadfence_block();   // the stores reach the wave's later loads of other lanes' entries
+          chunk_base = base;
+        }
       }
       const uint32_t avail = chunk_end - chunk_pos;
       const uint32_t rank = __popcll(m & lt_mask);
@@ -1780,14 +1974,17 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             rng.d = hsh; rng.x0 = hsh ^ 0x2c7f967fu; rng.x1 = hsh * 3u + 1u; rng.x2 = ~hsh;
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
           } else {
-            // tile-major states: the wave's lanes read consecutive words (256 B per state word)
-            const uint32_t n = A.n_ids, ri = tile * 64u + k;
-            rng.d = A.rng[ri]; rng.x0 = A.rng[n + ri]; rng.x1 = A.rng[2 * n + ri];
-            rng.x2 = A.rng[3 * n + ri]; rng.x3 = A.rng[4 * n + ri]; rng.x4 = A.rng[5 * n + ri];
+            // the state seeded at the chunk's pickup (the slot entry of this id)
+            const uint32_t so = (id - chunk_base) * 4u;
+            rng.d = A.rng_d;
+            rng.x0 = *reinterpret_cast<const uint32_t *>(rng_slot + so);
+            rng.x1 = *reinterpret_cast<const uint32_t *>(rng_slot + 256u + so);
+            rng.x2 = *reinterpret_cast<const uint32_t *>(rng_slot + 512u + so);
+            rng.x3 = *reinterpret_cast<const uint32_t *>(rng_slot + 768u + so);
+            rng.x4 = *reinterpret_cast<const uint32_t *>(rng_slot + 1024u + so);
           }
           sum = mk(0, 0, 0);
           sample = 0;
-          pixel_point();
           camera_ray();
         }
       }
@@ -1835,6 +2032,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     const bool tracing = busy && !pending;   // a lane still resuming its rejection keeps its hit
     Trace::template run<LDS, COUNT, UV>(S, A, tracing, __ballot(tracing), lane, stk, T, ray, h, vc);
     if (T.active) continue;                   // walk paused (verified traversal): resumes next round
+    if constexpr (lazy_hit<Trace>(0)) Trace::template materialize<LDS, UV>(S, A, T, ray, h);
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       ph_trace += t - t_mark; if (lone) lph[1] += t - t_mark;

@@ -36,6 +36,12 @@ enum : int {
 // 12/13 (kAccelLeaf | (count-1) << 24 | first prim, or a node index), per child at 14/15 an upper
 // bound M of |centre(t)| + radius over its spheres.  Prim = 16 words, in leaf order.
 constexpr int kAccelNodeWords = 16, kAccelPrimWords = 16;
+// 4-wide form of the same tree (accel::collapse_wide): a node = the 4 subtrees reached by opening the BVH2
+// child with the largest box twice; 32 words, structure-of-arrays so one 16-B load brings a plane of all four
+// children: x0[4] x1[4] y0[4] y1[4] z0[4] z1[4] at words 0..23 (the BVH2 child boxes, padding included), child
+// refs at 24..27 (kAccelLeaf leaf ref as in the BVH2, else a 4-wide node index), words 28..31 unused.  An empty
+// slot has the box (+inf, -inf) on every axis (never hit) and ref 0.
+constexpr int kAccel4NodeWords = 32, kAccel4Ref = 24;
 constexpr uint32_t kAccelLeaf = 0x80000000u;
 constexpr float kAccelKappa = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24): cone padding per unit of |oc|
 enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
@@ -172,8 +178,14 @@ struct RenderArgs {
   uint32_t rows;              // row_count
   uint32_t tiles_x;           // ceil(width / 8)
   uint32_t n_ids;             // 64 * ceil(rows/8) * tiles_x: tile-major pixel ids handed to waves
-  const uint32_t *rng;        // [6][n_ids] seeded XORWOW states {d, x0..x4}, tile-major (tile * 64 + k,
-                              // k = 8 * row-in-tile + column-in-tile): a wave's 64 pixels are 256 B per word
+  // RNG seeding fused into the tile pickup (init_gpu_data's curand_init, raytracing.cu:1591-1606): when a wave
+  // takes a chunk of pixel ids, lane l jumps the state of its pixel's row (rng_rows) over the pixel's column
+  // (binary jump through the nibble tables of P_k = J^(2^k), rng_nib) and leaves it in the wave's slot; the
+  // lanes that take those pixels read their states from there
+  const uint32_t *rng_rows;   // [rows][8] row base states {x0..x4, pad}: subsequence = global row * width
+  const uint32_t *rng_nib;    // kRngNibTableWords per power P_k (xorwow_jump.h kJumpNibbleOffset onwards)
+  uint32_t rng_d;             // the Weyl word d (the same for every subsequence)
+  uint32_t *rng_slot;         // per wave [5][64]: the states of the chunk of pixel ids it took last
   float *out;                 // [n_pixels][3]
   uint8_t *out8;              // optional [n_pixels][3] P6 payload bytes (pixels_to_ppm), null = none
   void *rc;                   // colour-stack levels past the LDS ones: [threads][max_bounces] codes
@@ -192,6 +204,7 @@ struct RenderArgs {
   uint32_t *fold_violation;       // folded traversal: set to 1 if a ray exceeded the host's bound
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
   uint32_t accel_nodes, accel_prims, accel_root;   // verified sphere traversal (word offsets, root node)
+  uint32_t accel_wide;            // word offset of the 4-wide nodes (kAccel4NodeWords each, root = node 0)
   uint32_t accel_lds_nodes;       // its first nodes (breadth-first: the top levels) staged at LDS word 0
   uint32_t *accel_fallbacks;      // rays the verified traversal handed to the reference walk (diagnostic)
   uint32_t defer_trace;           // verified traversal: the round's walk stops once at most this many
@@ -217,6 +230,11 @@ struct RenderArgs {
   // like a profiler's kernel duration and unlike stream events, never widened by neighbouring work
   unsigned long long *span;
 };
+
+// nibble table of a 160x160 GF(2) jump matrix (xorwow_jump.h): for input nibble c (bits 4c..4c+3 of the state)
+// and value v, the XOR of the rows of v's bits: words 0..3 as uint4 [c * 16 + v], then word 4 as u32 [c * 16 + v]
+constexpr uint32_t kRngNibTableWords = 40 * 16 * 5;
+constexpr uint32_t kRngSlotWords = 5 * 64;   // per wave
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)

@@ -31,6 +31,10 @@ struct SceneImage {
 struct SphereAccel {
   std::vector<uint32_t> node_words, prim_words;
   uint32_t root = 0, depth = 0, spheres = 0;
+  // the same tree 4 wide (accel::collapse_wide, rt_layout.h kAccel4*): root = node 0; wide_stack bounds the
+  // ordered walk's stack (up to 3 pushes per level)
+  std::vector<uint32_t> wide_words;
+  uint32_t wide_depth = 0, wide_stack = 0;
 };
 // false (with a reason) when the world is not an all-sphere BVH/group tree with >= min_spheres spheres
 bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel *out, std::string *why);

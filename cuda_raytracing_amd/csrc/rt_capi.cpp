@@ -148,16 +148,21 @@ struct rt_context {
   rt::SphereAccel accel;
   bool accel_ok = false;
   uint32_t accel_nodes = 0, accel_prims = 0;   // word offsets in the device image
+  uint32_t accel_wide = 0;                      // ... of the 4-wide nodes (0: none)
+  bool accel_w4 = false;                        // RT_ACCEL_WIDTH=4: the verified walk uses the 4-wide tree
   // top SAH nodes staged in LDS (RT_ACCEL_LDS_NODES): 64 (6 levels, 4 KiB per block) measured best on
   // the 10k scene, 1-3 % over none and over 128 / 256 (profiles/r03_ab_accel_lds_bfs_early*.jsonl)
   uint32_t accel_lds_nodes = 64;
+  bool accel_lds_set = false;   // RT_ACCEL_LDS_NODES given (nodes of the tree in use)
   // verified mixed-world traversal (RT_TRAV_MIXED): macro roots marked in the image, SAH words appended
   rt::MixedAccel mixed;
   bool mixed_ok = false;
   uint32_t mix_nodes = 0, mix_prims = 0;
   bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
   int static_ok = -1;          // the scene expands within jit_budget (straight-line, stackless traversal); -1 unknown
-  DevBuf scene, jump, rng, rc, work, counters, wave_trace, tile_cost, tile_order;
+  DevBuf scene, jump, rng_rows, rng_slot, rc, work, counters, wave_trace, tile_cost, tile_order;
+  // row base states of the last geometry (xorwow_row_bases), kept on the device: key = seed, W, rows of the shard
+  uint64_t rows_key[5] = {~0ull, 0, 0, 0, 0};
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
   bool counted = false;
@@ -237,6 +242,25 @@ int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_
   return RT_OK;
 }
 
+int rt_accel_build_wide(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]) {
+  if (!scene || !info) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  int st = rt::compile_scene(scene, &img);
+  if (st != RT_OK) return st;
+  rt::SphereAccel a;
+  std::string why;
+  if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why) || a.wide_words.empty()) return RT_ERR_UNSUPPORTED;
+  info[0] = static_cast<uint32_t>(a.wide_words.size() / rt::kAccel4NodeWords);
+  info[1] = a.wide_depth;
+  info[2] = a.wide_stack;
+  info[3] = static_cast<uint32_t>(a.wide_words.size());
+  if (words) {
+    if (cap < a.wide_words.size()) return RT_ERR_INVALID_ARG;
+    std::memcpy(words, a.wide_words.data(), a.wide_words.size() * 4);
+  }
+  return RT_OK;
+}
+
 int rt_mixed_build(const rt_scene *scene, uint32_t info[4]) {
   if (!scene || !info) return RT_ERR_INVALID_ARG;
   rt::SceneImage img;
@@ -278,7 +302,7 @@ void rt_context_destroy(rt_context *c) {
   {
     DeviceGuard g(c->device);
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
-    c->scene.release(); c->jump.release(); c->rng.release(); c->rc.release();
+    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_slot.release(); c->rc.release();
     c->work.release(); c->counters.release();
     c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
   }
@@ -322,7 +346,10 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_MIX_PROVE")) c->mix_no_proof = e[0] == '0';
-  if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+  if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
+    c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
+    c->accel_lds_set = true;
+  }
   int st = rt::compile_scene(scene, &c->img);
   if (st != RT_OK) { delete c; return st; }
   while (c->img.words.size() % 4) c->img.words.push_back(0);
@@ -344,6 +371,12 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     dev_words.insert(dev_words.end(), c->accel.node_words.begin(), c->accel.node_words.end());
     c->accel_prims = static_cast<uint32_t>(dev_words.size());
     dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
+    c->accel_w4 = rt::accel_width() == 4 && !c->accel.wide_words.empty();
+    if (c->accel_w4) {
+      while (dev_words.size() % 4) dev_words.push_back(0);
+      c->accel_wide = static_cast<uint32_t>(dev_words.size());
+      dev_words.insert(dev_words.end(), c->accel.wide_words.begin(), c->accel.wide_words.end());
+    }
   }
   if (c->mixed_ok) {
     c->mix_nodes = static_cast<uint32_t>(dev_words.size());
@@ -454,6 +487,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
   // (the mixed walk keeps a macro's SAH stack above the reference walk's entries)
   const uint32_t stack_cap = std::max({c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u,
+                                       c->accel_w4 ? c->accel.wide_stack : 0u,
                                        c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u});
   const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
   size_t stack_bytes = stackless ? 0 : full_stack_bytes;
@@ -530,7 +564,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (trav == RT_TRAV_ACCEL) {
     rt::JitKernels jk;
     std::string why;
-    if (rt::jit_accel_kernels(c->img, c->variant | trace_bit, &jk, &why)) {
+    if (rt::jit_accel_kernels(c->img, c->variant | trace_bit, c->accel_w4, &jk, &why)) {
       note_jit(jk);
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
@@ -560,16 +594,19 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // itself is not: they take the scene's place at the start of the block's LDS
   uint32_t accel_lds_nodes = 0;
   if (trav == RT_TRAV_ACCEL && !c->lds && c->accel_lds_nodes > 0) {
-    accel_lds_nodes = std::min<uint32_t>(c->accel_lds_nodes,
-                                         static_cast<uint32_t>(c->accel.node_words.size() / rt::kAccelNodeWords));
+    const uint32_t node_words = c->accel_w4 ? rt::kAccel4NodeWords : rt::kAccelNodeWords;
+    // the same LDS bytes either way by default (64 2-wide nodes = 32 4-wide ones); RT_ACCEL_LDS_NODES counts nodes
+    const uint32_t want = c->accel_lds_set ? c->accel_lds_nodes : c->accel_lds_nodes * rt::kAccelNodeWords / node_words;
+    accel_lds_nodes = std::min<uint32_t>(want, static_cast<uint32_t>((c->accel_w4 ? c->accel.wide_words.size()
+                                                                                  : c->accel.node_words.size()) / node_words));
     // only what the block's LDS budget leaves after the colour-stack levels and the stacks (an explicit
     // RT_RC_LDS_LEVELS may already take most of it): the staging shrinks, the launch never exceeds 160 KiB
     const bool nw = jit_fn != nullptr && narrow_ok;
     const size_t used = (nw ? ((rc_levels + 1) & ~1u) : rc_levels) * rc_level_bytes(nw) + stack_bytes + kLdsReserve;
-    const size_t node_bytes = static_cast<size_t>(rt::kAccelNodeWords) * 4;
+    const size_t node_bytes = static_cast<size_t>(node_words) * 4;
     const size_t room = used < kLdsPerCu ? (kLdsPerCu - used) / node_bytes : 0;
     accel_lds_nodes = static_cast<uint32_t>(std::min<size_t>(accel_lds_nodes, room));
-    scene_lds_words = accel_lds_nodes * rt::kAccelNodeWords;
+    scene_lds_words = accel_lds_nodes * node_words;
   }
   const bool narrow = jit_fn != nullptr && narrow_ok;   // the offline kernels use 32-bit codes
   const size_t level_bytes = rc_level_bytes(narrow);
@@ -612,7 +649,21 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
 
   const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
   const uint32_t n_ids = 64u * ((static_cast<uint32_t>(p->row_count) + 7) / 8) * tiles_x;
-  if (c->rng.ensure(static_cast<size_t>(n_ids) * 6 * 4) != hipSuccess) return RT_ERR_HIP;
+  // RNG: the row base states of this shard (host, once per geometry: a few ms; the 2M per-pixel jumps run in the
+  // render kernel at tile pickup) and the per-wave slots
+  {
+    const uint64_t key[5] = {p->seed, static_cast<uint64_t>(p->width), static_cast<uint64_t>(p->row_offset),
+                             static_cast<uint64_t>(p->row_stride), static_cast<uint64_t>(p->row_count)};
+    if (std::memcmp(key, c->rows_key, sizeof key) != 0) {
+      std::vector<uint32_t> rb;
+      rt::xorwow_row_bases(p->seed, p->width, p->row_offset, p->row_stride, p->row_count, &rb);
+      if (c->rng_rows.ensure(rb.size() * 4) != hipSuccess ||
+          hipMemcpy(c->rng_rows.p, rb.data(), rb.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return RT_ERR_HIP;
+      std::memcpy(c->rows_key, key, sizeof key);
+    }
+  }
+  if (c->rng_slot.ensure(static_cast<size_t>(threads / 64) * rt::kRngSlotWords * 4) != hipSuccess) return RT_ERR_HIP;
   if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;
   c->used_rc_levels = rc_levels;
   c->rc_audit_bytes = 0;
@@ -625,14 +676,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     if (hipMemsetAsync(c->rc.p, 0xff, c->rc_audit_bytes, s) != hipSuccess) return RT_ERR_HIP;
   }
 
-  rt::SeedArgs sa{};
-  sa.jump = static_cast<const uint32_t *>(c->jump.p);
-  rt::xorwow_seed_base(p->seed, sa.base);
-  sa.width = p->width; sa.row_offset = p->row_offset; sa.row_stride = p->row_stride;
-  sa.rows = static_cast<uint32_t>(p->row_count);
-  sa.tiles_x = tiles_x;
-  sa.n_ids = n_ids;
-  sa.rng = static_cast<uint32_t *>(c->rng.p);
+  uint32_t seed_base[6];
+  rt::xorwow_seed_base(p->seed, seed_base);
 
   rt::RenderArgs a{};
   a.scene = static_cast<const uint32_t *>(c->scene.p);
@@ -646,6 +691,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.accel_prims = c->accel_prims;
   a.accel_root = c->accel.root;
   a.accel_lds_nodes = accel_lds_nodes;
+  a.accel_wide = (trav == RT_TRAV_ACCEL && c->accel_w4) ? c->accel_wide : 0u;
   a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
   a.mix_nodes = c->mix_nodes;
   a.mix_prims = c->mix_prims;
@@ -669,7 +715,10 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.rows = static_cast<uint32_t>(p->row_count);
   a.tiles_x = tiles_x;
   a.n_ids = n_ids;
-  a.rng = static_cast<const uint32_t *>(c->rng.p);
+  a.rng_rows = static_cast<const uint32_t *>(c->rng_rows.p);
+  a.rng_nib = static_cast<const uint32_t *>(c->jump.p) + rt::kJumpNibbleOffset;
+  a.rng_d = seed_base[0];
+  a.rng_slot = static_cast<uint32_t *>(c->rng_slot.p);
   a.out = out_dev;
   a.out8 = out8_dev;
   a.rc = c->rc.p;
@@ -704,8 +753,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
 
   if (hipMemsetAsync(c->work.p, 0, 256, s) != hipSuccess) return RT_ERR_HIP;
   if (c->counted && hipMemsetAsync(c->counters.p, 0, RT_CNT__COUNT * 8, s) != hipSuccess) return RT_ERR_HIP;
+  // no seeding launch: the render kernel seeds each pixel's state at tile pickup (init_ms is the empty interval)
   if (hipEventRecord(c->ev[0], s) != hipSuccess) return RT_ERR_HIP;
-  if (rt::launch_seed(sa, s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[1], s) != hipSuccess) return RT_ERR_HIP;
   if (c->used_lpt) {
     // longest-first schedule: probe probe_per_tile throwaway 1-spp paths per tile (their own RNG,
@@ -722,7 +771,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     pa.spp = 1;
     pa.out = nullptr;
     pa.out8 = nullptr;
-    pa.rng = nullptr;
+    pa.rng_rows = nullptr;
+    pa.rng_slot = nullptr;
     pa.work = static_cast<uint32_t *>(c->work.p) + 8;
     pa.wave_trace = nullptr;
     pa.fold_violation = static_cast<uint32_t *>(c->work.p) + 14;   // probe rays: flag ignored
@@ -966,7 +1016,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     rt::SphereAccel a;
     std::string why;
     if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
-    src = rt::jit_accel_source(img, variant, rt::accel_waves());
+    src = rt::jit_accel_source(img, variant, rt::accel_waves(), rt::accel_width() == 4);
   } else if (traversal == RT_TRAV_MIXED) {
     rt::MixedAccel m;
     std::string why;
@@ -1026,6 +1076,19 @@ int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int
       const uint64_t id = ((lr >> 3) * tiles_x + (j >> 3)) * 64 + (lr & 7) * 8 + (j & 7);
       for (int w = 0; w < 6; ++w) out[w * n + lr * width + j] = tiled[w * n_ids + id];
     }
+  return RT_OK;
+}
+
+int rt_rng_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out) {
+  if (!out || width <= 0 || rows <= 0 || row_offset < 0 || row_stride <= 0) return RT_ERR_INVALID_ARG;
+  std::vector<uint32_t> rb;
+  rt::xorwow_row_bases(seed, width, row_offset, row_stride, rows, &rb);
+  uint32_t base[6];
+  rt::xorwow_seed_base(seed, base);
+  for (int k = 0; k < rows; ++k) {
+    out[k * 6] = base[0];
+    for (int w = 0; w < 5; ++w) out[k * 6 + 1 + w] = rb[static_cast<size_t>(k) * 8 + w];
+  }
   return RT_OK;
 }
 

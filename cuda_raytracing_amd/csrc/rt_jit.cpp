@@ -333,9 +333,9 @@ std::string waves_attr_n(int waves) {
   return waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : waves_attr();
 }
 
-std::string jit_accel_source(const SceneImage &img, int variant, int waves) {
+std::string jit_accel_source(const SceneImage &img, int variant, int waves, bool wide) {
   const int v = variant & kJitVarMask;
-  const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u>";
+  const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u, " + (wide ? "true" : "false") + ">";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr_n(waves) + " void rt_accel_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarNoProbe) + ", " + at + ">(A);\n}\n";
@@ -425,17 +425,23 @@ int accel_waves() {
   return 6;
 }
 
+// Width of the verified sphere walk's tree: 2 (the SAH BVH2) or 4 (its 4-wide collapse, accel::collapse_wide)
+int accel_width() {
+  if (const char *e = std::getenv("RT_ACCEL_WIDTH")) return std::atoi(e) == 4 ? 4 : 2;
+  return 2;
+}
+
 // The default 6-wave request is measured on the plain 10k walk, whose 80-VGPR build spills ~17 VGPRs outside
 // the node loop (44 B per lane).  Variants that need far more registers (noise, image u,v, deep bounces:
 // 125-149 VGPRs) would spill inside their hot loops; a default-request build with more scratch than this is
 // replaced by the allocator's own build (+ the residency raise).  An explicit RT_ACCEL_WAVES is kept as built.
 constexpr int kAccelWavesScratchMax = 96;
 
-bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
+bool jit_accel_kernels(const SceneImage &img, int variant, bool wide, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
   int w = accel_waves();
-  if (!build_module(jit_accel_source(img, variant, w), "rt_accel", out, why)) return false;
+  if (!build_module(jit_accel_source(img, variant, w, wide), "rt_accel", out, why)) return false;
   if (w > 0 && !std::getenv("RT_ACCEL_WAVES")) {
     int sc = 0;
     render_vgprs(out->render, &sc);
@@ -443,13 +449,13 @@ bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std:
       std::fprintf(stderr, "[rt] jit accel waves_per_eu(%d): scratch %d B per lane\n", w, sc);
     if (sc < 0 || sc > kAccelWavesScratchMax) {
       JitKernels k = *out;
-      if (!build_module(jit_accel_source(img, variant, 0), "rt_accel", &k, why)) return false;
+      if (!build_module(jit_accel_source(img, variant, 0, wide), "rt_accel", &k, why)) return false;
       k.ms += out->ms;
       *out = k;
       w = 0;
     }
   }
-  if (w == 0) raise_residency([&](int n) { return jit_accel_source(img, variant, n); }, "rt_accel", out);
+  if (w == 0) raise_residency([&](int n) { return jit_accel_source(img, variant, n, wide); }, "rt_accel", out);
   return true;
 }
 

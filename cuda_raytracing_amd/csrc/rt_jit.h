@@ -35,9 +35,11 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
 // kind dispatch of trav_step keeps only those branches).  Same contract as jit_kernels.
 bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
 std::string jit_lane_source(const SceneImage &img, int variant);
-// Verified sphere traversal kernels (AccelTraceK over the scene's node kinds for the fallback walk).
-bool jit_accel_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
-std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0);   // waves > 0: amdgpu_waves_per_eu
+// Verified sphere traversal kernels (AccelTraceK over the scene's node kinds for the fallback walk); wide: the
+// 4-wide tree (SphereAccel::wide_words)
+bool jit_accel_kernels(const SceneImage &img, int variant, bool wide, JitKernels *out, std::string *why);
+std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0, bool wide = false);   // waves > 0: amdgpu_waves_per_eu
+int accel_width();   // 2 or 4 (RT_ACCEL_WIDTH)
 int accel_waves();   // the verified sphere walk's waves per SIMD request (6; RT_ACCEL_WAVES, 0 = allocator's choice)
 // verified mixed-world traversal kernels (MixedTraceK over the scene's node kinds)
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);

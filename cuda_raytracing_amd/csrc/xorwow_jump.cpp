@@ -52,26 +52,67 @@ void build() {
     std::memcpy(a.r[b], v, sizeof v);
   }
   for (int i = 0; i < 67; ++i) { square(a, t); a = t; }
-  g_tables.resize(static_cast<size_t>(kJumpNibbleOffset) + kJumpNibbleWords);
+  g_tables.resize(static_cast<size_t>(kJumpNibbleOffset) + static_cast<size_t>(kJumpNibPowers) * kJumpNibbleWords);
   for (int k = 0; k < kJumpPowers; ++k) {
     std::memcpy(g_tables.data() + static_cast<size_t>(k) * kJumpMatrixWords, a.r, sizeof a.r);
     square(a, t);
     a = t;
   }
-  const uint32_t *p0 = g_tables.data();   // P_0, rows [b][word]
-  uint32_t *lo = g_tables.data() + kJumpNibbleOffset, *hi = lo + kJumpNibbles * 16 * 4;
-  for (int c = 0; c < kJumpNibbles; ++c)
-    for (int v = 0; v < 16; ++v) {
-      uint32_t r[5] = {0, 0, 0, 0, 0};
-      for (int i = 0; i < 4; ++i)
-        if ((v >> i) & 1)
-          for (int w = 0; w < 5; ++w) r[w] ^= p0[(4 * c + i) * 5 + w];
-      for (int w = 0; w < 4; ++w) lo[(c * 16 + v) * 4 + w] = r[w];
-      hi[c * 16 + v] = r[4];
-    }
+  for (int k = 0; k < kJumpNibPowers; ++k) {
+    const uint32_t *pk = g_tables.data() + static_cast<size_t>(k) * kJumpMatrixWords;   // P_k, rows [b][word]
+    uint32_t *lo = g_tables.data() + kJumpNibbleOffset + static_cast<size_t>(k) * kJumpNibbleWords;
+    uint32_t *hi = lo + kJumpNibbles * 16 * 4;
+    for (int c = 0; c < kJumpNibbles; ++c)
+      for (int v = 0; v < 16; ++v) {
+        uint32_t r[5] = {0, 0, 0, 0, 0};
+        for (int i = 0; i < 4; ++i)
+          if ((v >> i) & 1)
+            for (int w = 0; w < 5; ++w) r[w] ^= pk[(4 * c + i) * 5 + w];
+        for (int w = 0; w < 4; ++w) lo[(c * 16 + v) * 4 + w] = r[w];
+        hi[c * 16 + v] = r[4];
+      }
+  }
+}
+
+// M = the 160x160 matrix of x -> J^n x (rows[b] = image of e_b), by the binary powers P_k
+void power_matrix(const std::vector<uint32_t> &T, uint64_t n, Mat &m) {
+  for (int b = 0; b < 160; ++b) {
+    uint32_t v[5] = {0, 0, 0, 0, 0};
+    v[b >> 5] = 1u << (b & 31);
+    for (int k = 0; n >> k && k < kJumpPowers; ++k)
+      if ((n >> k) & 1u) apply(*reinterpret_cast<const Mat *>(T.data() + static_cast<size_t>(k) * kJumpMatrixWords), v);
+    std::memcpy(m.r[b], v, sizeof v);
+  }
 }
 
 }  // namespace
+
+void xorwow_jump_nib(const uint32_t *tables, int k, uint32_t x[5]) {
+  const uint32_t *lo = tables + kJumpNibbleOffset + static_cast<size_t>(k) * kJumpNibbleWords;
+  const uint32_t *hi = lo + kJumpNibbles * 16 * 4;
+  uint32_t r[5] = {0, 0, 0, 0, 0};
+  for (int c = 0; c < kJumpNibbles; ++c) {
+    const uint32_t e = c * 16 + ((x[c >> 3] >> (4 * (c & 7))) & 15u);
+    for (int w = 0; w < 4; ++w) r[w] ^= lo[e * 4 + w];
+    r[4] ^= hi[e];
+  }
+  std::memcpy(x, r, sizeof r);
+}
+
+void xorwow_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out) {
+  const std::vector<uint32_t> &T = xorwow_jump_tables();
+  out->assign(static_cast<size_t>(rows > 0 ? rows : 0) * 8, 0u);
+  if (rows <= 0) return;
+  uint32_t st[6];
+  xorwow_seed_host(seed, static_cast<uint64_t>(row_offset) * static_cast<uint64_t>(width), st);
+  uint32_t x[5] = {st[1], st[2], st[3], st[4], st[5]};
+  Mat m;
+  power_matrix(T, static_cast<uint64_t>(row_stride) * static_cast<uint64_t>(width), m);
+  for (int lr = 0; lr < rows; ++lr) {
+    std::memcpy(&(*out)[static_cast<size_t>(lr) * 8], x, sizeof x);
+    if (lr + 1 < rows) apply(m, x);
+  }
+}
 
 const std::vector<uint32_t> &xorwow_jump_tables() {
   std::call_once(g_once, build);

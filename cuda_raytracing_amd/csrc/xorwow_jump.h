@@ -14,7 +14,18 @@ constexpr int kJumpMatrixWords = 160 * 5;       // rows[b][k]: image of unit vec
 // as 640 uint4 [c * 16 + v], then word 4 as 640 u32.  P_0 x = XOR over c of table[c][nibble_c(x)].
 constexpr int kJumpNibbles = 40, kJumpNibbleWords = kJumpNibbles * 16 * 5;
 constexpr int kJumpNibbleOffset = kJumpPowers * kJumpMatrixWords;   // 16-B aligned (128 000 B)
+// Then the nibble tables of P_1 .. P_{kJumpNibPowers-1} in the same format, table k at
+// kJumpNibbleOffset + k * kJumpNibbleWords: the render kernel seeds a pixel from its row's base state by the
+// binary jump over its column index (columns < 2^kJumpNibPowers).
+constexpr int kJumpNibPowers = 31;
 const std::vector<uint32_t> &xorwow_jump_tables();
+
+// x <- P_k x through nibble table k (host)
+void xorwow_jump_nib(const uint32_t *tables, int k, uint32_t x[5]);
+// Row base states of a shard (the state of the row's first pixel, subsequence = global row index * width):
+// out[lr * 8 + w] = word x_w (w < 5) of global row row_offset + lr * row_stride, lr < rows.  The Weyl word d is
+// the same for every subsequence (xorwow_seed_base).
+void xorwow_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out);
 
 // Seeded state {d, x0..x4} for (seed, subsequence) — same as rocrand_init(seed, subsequence, 0).
 void xorwow_seed_host(uint64_t seed, uint64_t subsequence, uint32_t state[6]);

@@ -231,11 +231,20 @@ int rt_mixed_build(const rt_scene *scene, uint32_t info[4]);
  * receives the node words then the prim words (layout: device/rt_layout.h kAccel*).
  * RT_ERR_UNSUPPORTED when the world is not eligible. */
 int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
+/* The same tree 4 wide (the verified walk's RT_ACCEL_WIDTH=4 form, device/rt_layout.h kAccel4*; no device
+ * needed): info = {wide nodes, depth, stack bound of the ordered walk, node words}; words (if non-null, cap
+ * words) receives the node words.  RT_ERR_UNSUPPORTED when the world is not eligible. */
+int rt_accel_build_wide(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
 /* The per-pixel XORWOW states rt_render seeds on the device (init_gpu_data's curand_init,
  * raytracing.cu:1591-1606, subsequence = global pixel index), for rows row_offset + k*row_stride,
  * k < rows, of a width-wide frame: out_states (host) receives [6][rows*width] words {d, x0..x4}.
  * Diagnostics/tests: the render path seeds into device memory and never copies the states back. */
 int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out_states);
+/* The row base states the render seeds its pixels from (no device needed; tests): for rows row_offset +
+ * k*row_stride, k < rows, of a width-wide frame, out (rows*6 words) receives {d, x0..x4} of the state of the
+ * row's first pixel (subsequence = global row * width).  The render kernel jumps each pixel's state from its
+ * row's over the column index at tile pickup (RenderArgs::rng_rows). */
+int rt_rng_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out);
 /* Last fallback reason of a context (why RT_TRAV_STATIC was not used); "" if none. */
 const char *rt_context_note(const rt_context *ctx);
 

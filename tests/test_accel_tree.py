@@ -122,3 +122,44 @@ def test_verification_boxes_are_reference_ancestors(idx):
 def test_other_worlds_are_not_eligible(idx):
     w, _ = rt.build_scene(idx)
     assert rt.accel_build(w.scene()) is None
+
+
+@pytest.mark.parametrize("idx", [2, rt.RT_SCENE_RANDOM_10K])
+def test_wide_tree_is_the_same_tree_four_wide(idx):
+    # accel::collapse_wide: every BVH2 leaf appears once among the wide nodes' children, each with its BVH2
+    # (padded) box; inner children are wide nodes numbered breadth-first; empty slots never hit
+    w, _ = rt.build_scene(idx)
+    info, nodes2, _ = rt.accel_build(w.scene())
+    wide = rt.accel_build_wide(w.scene())
+    assert wide is not None
+    winfo, wn = wide
+    wn = wn.reshape(-1, 32)
+    nodes2 = nodes2.reshape(-1, 16)
+    leaves2 = {}
+    for q in nodes2:
+        for c in range(2):
+            if int(q[12 + c]) & LEAF:
+                leaves2[int(q[12 + c])] = tuple(q[6 * c: 6 * c + 6])
+    leaves4 = {}
+    kids = []
+    for i, q in enumerate(wn):
+        for c in range(4):
+            ref = int(q[24 + c])
+            box = tuple(int(q[4 * k + c]) for k in range(6))
+            bf = f(np.array(box, np.uint32))
+            if ref & LEAF:
+                assert ref not in leaves4
+                leaves4[ref] = tuple(np.array(box, np.uint32))
+            elif np.isinf(bf[0]) and bf[0] > 0:   # empty slot: (+inf, -inf) on every axis
+                assert ref == 0 and all(np.isinf(bf))
+            else:
+                kids.append(ref)
+                inner = wn[ref]
+                for cc in range(4):   # the child's own child boxes lie inside this box
+                    ib = f(np.array([inner[4 * k + cc] for k in range(6)], np.uint32))
+                    if np.isinf(ib[0]) and ib[0] > 0:
+                        continue
+                    assert np.all(bf[0::2] <= ib[0::2]) and np.all(bf[1::2] >= ib[1::2])
+    assert {k: tuple(np.array(v, np.uint32)) for k, v in leaves2.items()} == leaves4
+    assert kids == list(range(1, len(wn)))   # breadth-first
+    assert winfo["stack"] == 3 * winfo["depth"] + 1 and winfo["depth"] <= info["depth"]

@@ -999,3 +999,41 @@ def test_kernel_span_within_event_window():
     cam, W, H = rt.camera_from_settings(s, 320, 180)
     fb, st = gpu(w.scene(), cam, rt.make_params(s, W, H, spp=16, bounces=8))
     assert 0 < st.render_kernel_ms <= st.render_ms * 1.001 + 0.01, (st.render_kernel_ms, st.render_ms)
+
+
+# ---- the verified sphere walk over the 4-wide tree (RT_ACCEL_WIDTH=4, accel::collapse_wide) ----
+@pytest.mark.parametrize("idx,W,H,spp", [(2, 64, 36, 4), (20, 160, 90, 6), (20, 480, 270, 4)])
+def test_wide_verified_sphere_traversal_matches_oracle(idx, W, H, spp, monkeypatch):
+    monkeypatch.setenv("RT_ACCEL_WIDTH", "4")
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL)
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_ACCEL and st.accel_spheres > 0
+    if W * H <= 160 * 90:
+        rc, ref, _ = oracle_render(w.scene(), cam, p)
+        assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+    else:
+        _rows_match_oracle(w, s, cam, W, H, spp, 16, fb, 7)
+    # counters: the same reference visits, the 4-wide walk's own executed steps
+    pc = rt.make_params(s, W, H, spp=2, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL | rt.RT_FLAG_COUNT)
+    _, sc4 = gpu(w.scene(), cam, pc)
+    monkeypatch.setenv("RT_ACCEL_WIDTH", "2")
+    _, sc2 = gpu(w.scene(), cam, pc)
+    a, b = sc4.counter_dict(), sc2.counter_dict()
+    assert a["visit_bvh"] == b["visit_bvh"] and a["visit_sphere"] == b["visit_sphere"]
+    assert 0 < a["exec_node"] and 0 < a["exec_prim"]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4, 5])
+def test_wide_random_sphere_worlds_verified_walk(seed, monkeypatch):
+    monkeypatch.setenv("RT_ACCEL_WIDTH", "4")
+    w, s = _random_sphere_world(seed)
+    cam, W, H = rt.camera_from_settings(s, 64, 36)
+    p = rt.make_params(s, W, H, spp=4, bounces=12)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    p.flags = rt.RT_FLAG_FORCE_ACCEL
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_ACCEL
+    assert np.array_equal(bits(fb), bits(ref))

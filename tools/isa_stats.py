@@ -21,7 +21,7 @@ sys.path.insert(0, str(REPO))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("scene", type=int)
-    ap.add_argument("--trav", default="static", choices=("static", "accel", "lane"))
+    ap.add_argument("--trav", default="static", choices=("static", "accel", "lane", "mixed"))
     ap.add_argument("--bounces", type=int, default=16)
     ap.add_argument("--out", default="/tmp/isa")
     ap.add_argument("--flags", default="")
@@ -29,7 +29,7 @@ def main():
     import cuda_raytracing_amd as rt
     from cuda_raytracing_amd import _abi
     w, _ = rt.build_scene(a.scene)
-    trav = {"static": rt.RT_TRAV_STATIC, "accel": rt.RT_TRAV_ACCEL, "lane": rt.RT_TRAV_LANE}[a.trav]
+    trav = {"static": rt.RT_TRAV_STATIC, "accel": rt.RT_TRAV_ACCEL, "lane": rt.RT_TRAV_LANE, "mixed": rt.RT_TRAV_MIXED}[a.trav]
     buf = C.create_string_buffer(1 << 24)
     rc = _abi.hip_lib().rt_kernel_source(C.byref(w.scene()), trav, a.bounces, buf, len(buf))
     if rc != 0:
