@@ -8,8 +8,8 @@
 A "step" is one frame, rendered to completion before the next starts (the frames run one after the other
 on one stream; the host enqueues the next frame while the GPU renders the current one, so no host
 round trip sits between them) — the reference's metric is one
-cuda_calc launch (raytracing.cu:1752-1768): RNG seeding + longest-first schedule probe + render kernel
-writing float RGB and PPM bytes (+ the RCCL gather of the u8 rows to rank 0 when N>1), with the scene
+cuda_calc launch (raytracing.cu:1752-1768) with init_gpu_data's seeding (:1746): longest-first schedule probe +
+render kernel (RNG seeding fused into its tile pickup) writing float RGB and PPM bytes (+ the RCCL gather of the u8 rows to rank 0 when N>1), with the scene
 already resident in HBM.  Default workload = BASELINE config 2: scene 0 (fv1) at 1920x1080, spp 512,
 depth 16 on one GPU.  With N ranks (torch.distributed.run, one process per GPU, backend "nccl" = RCCL)
 rows are interleaved across ranks and
@@ -454,7 +454,7 @@ def main():
                 "scene": args.scene, "width": W, "height": H, "spp": args.spp, "bounces": args.bounces,
                 "frame": args.frame,
                 "parallelism": f"rows interleaved x{world_size}" + ((" + RCCL u8 gather" if args.dist_backend == "nccl" else f" + {args.dist_backend} u8 gather") if world_size > 1 else ""),
-                "step": "one frame to completion: RNG seed + schedule probe + render (float RGB + PPM bytes); "
+                "step": "one frame to completion: schedule probe + render (RNG seeding at tile pickup, float RGB + PPM bytes); "
                         "frames in order on one stream, the host one frame ahead"
                         + (" + gather to rank 0" if world_size > 1 else ""),
                 "pixels_per_gpu": rows * W,

@@ -352,16 +352,18 @@ def accel_build(scene: Scene):
     return {"root": info[0], "depth": info[1], "spheres": info[2]}, buf[:nw], buf[nw:]
 
 
-def accel_build_wide(scene: Scene):
-    """4-wide form of the verified walk's tree (no device needed): (info dict, node words as uint32), or None."""
+def accel_build_wide(scene: Scene, quant: bool = False):
+    """4-wide form of the verified walk's tree (no device needed): (info dict, node words as uint32), or None.
+    quant: the quantised 64-B nodes (rt_accel_build_quant) instead of the float 128-B ones."""
     L = _abi.hip_lib()
+    fn = L.rt_accel_build_quant if quant else L.rt_accel_build_wide
     info = (C.c_uint32 * 4)()
-    rc = L.rt_accel_build_wide(C.byref(scene), None, 0, info)
+    rc = fn(C.byref(scene), None, 0, info)
     if rc == _abi.RT_ERR_UNSUPPORTED:
         return None
-    _check(rc, "rt_accel_build_wide")
+    _check(rc, fn.__name__)
     buf = np.zeros(info[3], np.uint32)
-    _check(L.rt_accel_build_wide(C.byref(scene), buf.ctypes.data_as(C.c_void_p), len(buf), info), "rt_accel_build_wide")
+    _check(fn(C.byref(scene), buf.ctypes.data_as(C.c_void_p), len(buf), info), fn.__name__)
     return {"nodes": info[0], "depth": info[1], "stack": info[2]}, buf
 
 

@@ -243,5 +243,69 @@ inline std::vector<uint32_t> collapse_wide(const std::vector<uint32_t> &nodes, u
   return out;
 }
 
+// Quantised 4-wide nodes (rt_layout.h kAccel4Q*) from collapse_wide's nodes, same numbering.  Per node and axis:
+// the origin o = the valid children's lowest plane minus the rounding pad ep (= 2^-20 of the node's largest
+// |plane| on the axis), rounded down to a float; the step 2^e the smallest power of two whose 255 steps reach the
+// highest plane plus ep; each child plane rounded outward to a step (q_lo = floor, q_hi = ceil, checked in exact
+// double arithmetic), so every decoded box contains its float box widened by ep.  Returns false (out cleared)
+// when a step would leave the exponent range the kernel's scale 2^e / d tolerates (|e| <= 40).
+inline bool quantize_wide(const std::vector<uint32_t> &wide, std::vector<uint32_t> *out) {
+  const size_t n = wide.size() / kAccel4NodeWords;
+  out->assign(n * kAccel4QNodeWords, 0u);
+  for (size_t i = 0; i < n; ++i) {
+    const uint32_t *w = &wide[i * kAccel4NodeWords];
+    uint32_t *o = &(*out)[i * kAccel4QNodeWords];
+    uint32_t valid = 0;
+    for (int c = 0; c < 4; ++c) {
+      bool ok = true;
+      for (int a = 0; a < 3; ++a) ok = ok && fl(w[(2 * a) * 4 + c]) <= fl(w[(2 * a + 1) * 4 + c]);
+      if (ok) valid |= 1u << c;
+    }
+    uint32_t meta = valid << 24;
+    for (int a = 0; a < 3; ++a) {
+      double lo = std::numeric_limits<double>::infinity(), hi = -lo;
+      for (int c = 0; c < 4; ++c)
+        if (valid >> c & 1u) { lo = std::min(lo, static_cast<double>(fl(w[(2 * a) * 4 + c]))); hi = std::max(hi, static_cast<double>(fl(w[(2 * a + 1) * 4 + c]))); }
+      if (!valid) lo = hi = 0.0;
+      if (!std::isfinite(lo) || !std::isfinite(hi)) { out->clear(); return false; }
+      const double ep = std::max(std::fabs(lo), std::fabs(hi)) * 0x1p-20;
+      float org = static_cast<float>(lo - ep);
+      while (static_cast<double>(org) > lo - ep) org = std::nextafter(org, -std::numeric_limits<float>::infinity());
+      const double ext = (hi + ep) - static_cast<double>(org);
+      int e = ext > 0 ? static_cast<int>(std::ceil(std::log2(ext / 255.0))) : -40;
+      e = std::max(e, -40);
+      uint32_t qlo = 0, qhi = 0;
+      for (;; ++e) {
+        if (e > 40) { out->clear(); return false; }
+        const double step = std::ldexp(1.0, e);
+        bool fits = true;
+        qlo = qhi = 0;
+        for (int c = 0; c < 4 && fits; ++c) {
+          uint32_t l = 255, h = 0;   // empty slot: never tested (valid mask)
+          if (valid >> c & 1u) {
+            const double clo = static_cast<double>(fl(w[(2 * a) * 4 + c])) - ep, chi = static_cast<double>(fl(w[(2 * a + 1) * 4 + c])) + ep;
+            double ql = std::floor((clo - org) / step), qh = std::ceil((chi - org) / step);
+            while (ql > 0 && org + ql * step > clo) ql -= 1;
+            while (org + qh * step < chi) qh += 1;
+            if (ql < 0 || qh > 255) { fits = false; break; }
+            l = static_cast<uint32_t>(ql);
+            h = static_cast<uint32_t>(qh);
+          }
+          qlo |= l << (8 * c);
+          qhi |= h << (8 * c);
+        }
+        if (fits) break;
+      }
+      o[a] = fb(org);
+      meta |= static_cast<uint32_t>(e + 127) << (8 * a);
+      o[4 + 2 * a] = qlo;
+      o[5 + 2 * a] = qhi;
+    }
+    o[3] = meta;
+    for (int c = 0; c < 4; ++c) o[kAccel4QRef + c] = w[kAccel4Ref + c];
+  }
+  return true;
+}
+
 }  // namespace accel
 }  // namespace rt

@@ -915,7 +915,11 @@ __device__ __forceinline__ void sort4(uint32_t &a, uint32_t &b, uint32_t &c, uin
 // the others pushed far to near, the spheres of every hit leaf child tested in the step (one per-lane loop).
 // Every sphere is culled by exactly the box the 2-wide walk would test for it, so the record, the tie flag and
 // the reach proof are those of the 2-wide walk.
-template <uint32_t KM, bool W4 = false>
+// Q: the quantised 4-wide nodes (rt_layout.h kAccel4Q*, accel::quantize_wide): one 64-B line per node, the planes
+// as bytes over a per-axis origin and power-of-two step; plane t = fma(q, 2^e / d, fma(o, 1/d, on)) — the boxes
+// contain the float ones widened for this evaluation's rounding, so the culling stays conservative (any tree
+// that reaches every sphere the reference could accept gives the same record: the verified walk above).
+template <uint32_t KM, bool W4 = false, bool Q = false>
 struct AccelTraceK {
   template <bool LDS, bool COUNT, bool UV>
   __device__ __forceinline__ static void run(const Mem<LDS> &S, const RenderArgs &A, bool busy, uint64_t lanes,
@@ -974,31 +978,60 @@ struct AccelTraceK {
           // immediate offsets (LDS for the staged top of the tree, else global: two explicit loads, not a flat one)
           // (address-space-typed pointers: merged into one generic pointer, the two paths become flat loads)
           typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-          u32x4 v[7];
+          constexpr int NV = Q ? 4 : 7, NS = Q ? 4 : 8;
+          u32x4 v[NV];
           if (node < A.accel_lds_nodes) {
             const __attribute__((address_space(3))) u32x4 *L =
-                (const __attribute__((address_space(3))) u32x4 *)(static_cast<uintptr_t>(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(g_lds)))) + node * 8;
+                (const __attribute__((address_space(3))) u32x4 *)(static_cast<uintptr_t>(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(g_lds)))) + node * NS;
 #pragma unroll
-            for (int k = 0; k < 7; ++k) v[k] = L[k];
+            for (int k = 0; k < NV; ++k) v[k] = L[k];
           } else {
             const __attribute__((address_space(1))) u32x4 *G =
-                (const __attribute__((address_space(1))) u32x4 *)(reinterpret_cast<uintptr_t>(N)) + node * 8;
+                (const __attribute__((address_space(1))) u32x4 *)(reinterpret_cast<uintptr_t>(N)) + node * NS;
 #pragma unroll
-            for (int k = 0; k < 7; ++k) v[k] = G[k];
+            for (int k = 0; k < NV; ++k) v[k] = G[k];
           }
+          if (COUNT) vc.xn += 2;   // four boxes: two 2-wide steps' worth (the op model's per-step weight)
+          uint32_t key[4], cnt[4], rr[4];
+          if constexpr (Q) {
+            // per axis: scale 2^e / d and the offsets fma(o, 1/d, on / of); near / far plane bytes by the octant
+            const uint32_t meta = v[0].w;
+            const float sx = __builtin_amdgcn_ldexpf(T.inv.x, static_cast<int>(meta & 0xffu) - 127);
+            const float sy = __builtin_amdgcn_ldexpf(T.inv.y, static_cast<int>((meta >> 8) & 0xffu) - 127);
+            const float sz = __builtin_amdgcn_ldexpf(T.inv.z, static_cast<int>((meta >> 16) & 0xffu) - 127);
+            const float bnx = __builtin_fmaf(asf(v[0].x), T.inv.x, sr.on.x), bfx = __builtin_fmaf(asf(v[0].x), T.inv.x, sr.of.x);
+            const float bny = __builtin_fmaf(asf(v[0].y), T.inv.y, sr.on.y), bfy = __builtin_fmaf(asf(v[0].y), T.inv.y, sr.of.y);
+            const float bnz = __builtin_fmaf(asf(v[0].z), T.inv.z, sr.on.z), bfz = __builtin_fmaf(asf(v[0].z), T.inv.z, sr.of.z);
+            const uint32_t xn = sr.nx ? v[1].y : v[1].x, xf = sr.nx ? v[1].x : v[1].y;
+            const uint32_t yn = sr.ny ? v[1].w : v[1].z, yf = sr.ny ? v[1].z : v[1].w;
+            const uint32_t zn = sr.nz ? v[2].y : v[2].x, zf = sr.nz ? v[2].x : v[2].y;
+            rr[0] = v[2].z; rr[1] = v[2].w; rr[2] = v[3].x; rr[3] = v[3].y;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const float tnx = __builtin_fmaf(static_cast<float>((xn >> (8 * c)) & 0xffu), sx, bnx);
+              const float tfx = __builtin_fmaf(static_cast<float>((xf >> (8 * c)) & 0xffu), sx, bfx);
+              const float tny = __builtin_fmaf(static_cast<float>((yn >> (8 * c)) & 0xffu), sy, bny);
+              const float tfy = __builtin_fmaf(static_cast<float>((yf >> (8 * c)) & 0xffu), sy, bfy);
+              const float tnz = __builtin_fmaf(static_cast<float>((zn >> (8 * c)) & 0xffu), sz, bnz);
+              const float tfz = __builtin_fmaf(static_cast<float>((zf >> (8 * c)) & 0xffu), sz, bfz);
+              const float t0 = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, kTmin)), t1 = fminf(fminf(tfx, tfy), fminf(tfz, T.tmax));
+              const bool hit = !(t1 < t0) && ((meta >> (24 + c)) & 1u);
+              const bool leaf = (rr[c] & kAccelLeaf) != 0;
+              key[c] = (hit && !leaf) ? ((__float_as_uint(t0) & 0xffff0000u) | rr[c]) : 0xffffffffu;
+              cnt[c] = (hit && leaf) ? ((rr[c] >> 24) & 0x7fu) + 1u : 0u;
+            }
+          } else {
           const uint4 X0 = make_uint4(v[0].x, v[0].y, v[0].z, v[0].w), X1 = make_uint4(v[1].x, v[1].y, v[1].z, v[1].w);
           const uint4 Y0 = make_uint4(v[2].x, v[2].y, v[2].z, v[2].w), Y1 = make_uint4(v[3].x, v[3].y, v[3].z, v[3].w);
           const uint4 Z0 = make_uint4(v[4].x, v[4].y, v[4].z, v[4].w), Z1 = make_uint4(v[5].x, v[5].y, v[5].z, v[5].w);
-          const uint4 R4 = make_uint4(v[6].x, v[6].y, v[6].z, v[6].w);
+          const uint4 R4 = make_uint4(v[NV - 1].x, v[NV - 1].y, v[NV - 1].z, v[NV - 1].w);
           // near / far plane per axis by the ray's octant (the near plane is the max one when 1/d < 0)
           const uint4 XN = sr.nx ? X1 : X0, XF = sr.nx ? X0 : X1, YN = sr.ny ? Y1 : Y0, YF = sr.ny ? Y0 : Y1;
           const uint4 ZN = sr.nz ? Z1 : Z0, ZF = sr.nz ? Z0 : Z1;
-          if (COUNT) vc.xn += 2;   // four boxes: two 2-wide steps' worth (the op model's per-step weight)
           const uint32_t xn[4] = {XN.x, XN.y, XN.z, XN.w}, xf[4] = {XF.x, XF.y, XF.z, XF.w};
           const uint32_t yn[4] = {YN.x, YN.y, YN.z, YN.w}, yf[4] = {YF.x, YF.y, YF.z, YF.w};
           const uint32_t zn[4] = {ZN.x, ZN.y, ZN.z, ZN.w}, zf[4] = {ZF.x, ZF.y, ZF.z, ZF.w};
-          const uint32_t rr[4] = {R4.x, R4.y, R4.z, R4.w};
-          uint32_t key[4], cnt[4];
+          rr[0] = R4.x; rr[1] = R4.y; rr[2] = R4.z; rr[3] = R4.w;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             // accel_box with the planes already in near / far order
@@ -1012,6 +1045,7 @@ struct AccelTraceK {
             // with the node index in the low 16 bits (only the visit order depends on the truncation)
             key[c] = (hit && !leaf) ? ((__float_as_uint(t0) & 0xffff0000u) | rr[c]) : 0xffffffffu;
             cnt[c] = (hit && leaf) ? ((rr[c] >> 24) & 0x7fu) + 1u : 0u;
+          }
           }
           // the hit leaves' spheres, in one per-lane loop below: sphere k of the concatenated ranges
           const uint32_t p1 = cnt[0], p2 = p1 + cnt[1], p3 = p2 + cnt[2], tot = p3 + cnt[3];
@@ -1733,10 +1767,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
     for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
     __syncthreads();
-  } else if (A.accel_lds_nodes) {   // the verified walk's top nodes (4 uint4 each; 8 in the 4-wide tree)
+  } else if (A.accel_lds_nodes) {   // the verified walk's top nodes (A.accel_node_u4 uint4 each)
     const uint4 *src = reinterpret_cast<const uint4 *>(A.scene + (A.accel_wide ? A.accel_wide : A.accel_nodes));
     uint4 *dst = reinterpret_cast<uint4 *>(g_lds);
-    const uint32_t n4 = A.accel_lds_nodes * (A.accel_wide ? 8u : 4u);
+    const uint32_t n4 = A.accel_lds_nodes * A.accel_node_u4;
     for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
     __syncthreads();
   }
@@ -1748,15 +1782,20 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   // wide: rcw[k * 64]; narrow: two levels per word, rch[(k >> 1) * 128 + (k & 1)] (rc_lds_levels even) —
   // deeper levels in HBM at rc[gtid * max_bounces + k]
   constexpr bool WIDE = (F & kVarNarrow) == 0;
+  constexpr bool BYTE = !WIDE && (F & kVarByte) != 0;   // 8-bit codes: four levels per word, rcb[(k >> 2) * 256 + (k & 3)]
+  constexpr bool RC_LDS = (F & kVarRcLds) != 0;          // every level in LDS (host-checked): no HBM level code
   const uint32_t mb = static_cast<uint32_t>(A.max_bounces);
   uint32_t *rcw = g_lds + A.rc_lds_word + wave * A.rc_lds_levels * 64 + lane;
   uint16_t *rch = reinterpret_cast<uint16_t *>(g_lds + A.rc_lds_word + wave * (A.rc_lds_levels >> 1) * 64 + lane);
+  uint8_t *rcb = reinterpret_cast<uint8_t *>(g_lds + A.rc_lds_word + wave * (A.rc_lds_levels >> 2) * 64 + lane);
   auto rc_lds_store = [&](uint32_t k, uint32_t code) {
     if (WIDE) rcw[k * 64] = code;
+    else if (BYTE) rcb[(k >> 2) * 256 + (k & 3)] = static_cast<uint8_t>(code);
     else rch[(k >> 1) * 128 + (k & 1)] = static_cast<uint16_t>(code);
   };
   auto rc_lds_load = [&](uint32_t k) -> uint32_t {
-    return WIDE ? rcw[k * 64] : static_cast<uint32_t>(rch[(k >> 1) * 128 + (k & 1)]);
+    return WIDE ? rcw[k * 64] : (BYTE ? static_cast<uint32_t>(rcb[(k >> 2) * 256 + (k & 3)])
+                                      : static_cast<uint32_t>(rch[(k >> 1) * 128 + (k & 1)]));
   };
   // HBM levels lane-contiguous (rc[gtid * max_bounces + k]): a deep path's successive levels fill the same
   // cache lines, which reach HBM whole instead of as one 4-byte piece per line
@@ -1770,11 +1809,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   auto rc_hbm_store = [&](uint32_t k, uint32_t code) {
     const size_t i = rc_at(k);
     if (WIDE) static_cast<uint32_t *>(A.rc)[i] = code;
+    else if (BYTE) static_cast<uint8_t *>(A.rc)[i] = static_cast<uint8_t>(code);
     else static_cast<uint16_t *>(A.rc)[i] = static_cast<uint16_t>(code);
   };
   auto rc_hbm_load = [&](uint32_t k) -> uint32_t {
     const size_t i = rc_at(k);
-    return WIDE ? static_cast<const uint32_t *>(A.rc)[i] : static_cast<uint32_t>(static_cast<const uint16_t *>(A.rc)[i]);
+    return WIDE ? static_cast<const uint32_t *>(A.rc)[i]
+                : (BYTE ? static_cast<uint32_t>(static_cast<const uint8_t *>(A.rc)[i])
+                        : static_cast<uint32_t>(static_cast<const uint16_t *>(A.rc)[i]));
   };
   const uint64_t lt_mask = (1ull << lane) - 1ull;
 
@@ -1913,11 +1955,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         chunk_end = min(base + size, A.n_ids);
         if (!probe) {
           // RNG seeding of the chunk (init_gpu_data's curand_init, :1591-1606, subsequence = global pixel index
-          // i * W + j): lane l takes id base + l, starts from the state of its row (row base, subsequence i * W)
-          // and jumps over the column j by the binary powers P_k = J^(2^k) (bits >= 3 of j are the tile column,
-          // wave-uniform); the states wait in the wave's slot for the lanes that take those pixels
+          // i * W + j): lane l takes id base + l, starts from the phase base of its pixel (the row's state jumped
+          // over the column's low 3 bits, host) and applies the column table of its tile column (J^(8 (j >> 3))):
+          // one nibble-table product per lane, the same table across the wave; the states wait in the wave's
+          // slot for the lanes that take those pixels
           const uint32_t id = base + lane;
-          uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0, jcol = 0;
+          uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0, tcol = 0;
           if (id < chunk_end) {
             uint32_t tile = id >> 6;
             const uint32_t kk = id & 63u;
@@ -1925,15 +1968,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
             const uint32_t lr = ty * 8 + (kk >> 3), j = tx * 8 + (kk & 7u);
             if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
-              const uint4 rb = *reinterpret_cast<const uint4 *>(A.rng_rows + lr * 8);
-              x0 = rb.x; x1 = rb.y; x2 = rb.z; x3 = rb.w; x4 = A.rng_rows[lr * 8 + 4];
-              jcol = j;
+              const uint32_t *pb = A.rng_rows + (lr * 8 + (kk & 7u)) * 8;
+              const uint4 rb = *reinterpret_cast<const uint4 *>(pb);
+              x0 = rb.x; x1 = rb.y; x2 = rb.z; x3 = rb.w; x4 = pb[4];
+              tcol = tx;
             }
           }
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(A.rng_nib), 0,
                                                                               0x7fffffff, 0x00020000);
-          for (uint32_t b = 0; __ballot((jcol >> b) != 0u) != 0; ++b)
-            if ((jcol >> b) & 1u) rng_jump_nib(rs, b * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
+          rng_jump_nib(rs, tcol * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
           *reinterpret_cast<uint32_t *>(rng_slot + lane * 4u) = x0;
           *reinterpret_cast<uint32_t *>(rng_slot + 256u + lane * 4u) = x1;
           *reinterpret_cast<uint32_t *>(rng_slot + 512u + lane * 4u) = x2;
@@ -2178,7 +2221,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         // push the attenuation's code (the emission pushed with it is always 0: only lights emit and
         // lights never scatter, raytracing.cu:439-450 vs :457-488, so the unwind adds +0.0f per level)
         if (push) {
-          if (rsp < A.rc_lds_levels) rc_lds_store(rsp, code);
+          if (RC_LDS || rsp < A.rc_lds_levels) rc_lds_store(rsp, code);
           else rc_hbm_store(rsp, code);
           rsp++;
         }
@@ -2215,7 +2258,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       // decoded together, ahead of the multiply chain (one memory latency per batch, not per level)
       int32_t k = static_cast<int32_t>(rsp) - 1;
       const int32_t kl = static_cast<int32_t>(A.rc_lds_levels);
-      while (k >= kl) {
+      while (!RC_LDS && k >= kl) {
         constexpr int kUnwindBatch = DEEP ? RT_UNWIND_BATCH : 1;
         uint32_t cw[kUnwindBatch];
 #pragma unroll

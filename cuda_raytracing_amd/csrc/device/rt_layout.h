@@ -42,6 +42,13 @@ constexpr int kAccelNodeWords = 16, kAccelPrimWords = 16;
 // refs at 24..27 (kAccelLeaf leaf ref as in the BVH2, else a 4-wide node index), words 28..31 unused.  An empty
 // slot has the box (+inf, -inf) on every axis (never hit) and ref 0.
 constexpr int kAccel4NodeWords = 32, kAccel4Ref = 24;
+// Quantised form of the 4-wide tree (accel::quantize_wide; RT_ACCEL_QUANT): 16 words, one 64-B line per node.
+// Words 0..2 = the node's origin o_a (float), word 3 = the per-axis scale exponents e_a + 127 in bytes 0..2 and
+// the valid-child mask in bits 24..27; words 4..9 = the planes as bytes (byte c = child c): x_lo x_hi y_lo y_hi
+// z_lo z_hi, plane = o_a + q * 2^e_a; words 10..13 = the child refs (as kAccel4Ref); words 14..15 unused.  Each
+// decoded box contains the float child box, itself widened by 2^-20 of the node's largest magnitude on that axis
+// (the rounding of the fma(q, 2^e / d, fma(o, 1/d, -o_ray / d)) evaluation), so the culling stays conservative.
+constexpr int kAccel4QNodeWords = 16, kAccel4QRef = 10;
 constexpr uint32_t kAccelLeaf = 0x80000000u;
 constexpr float kAccelKappa = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24): cone padding per unit of |oc|
 enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
@@ -141,8 +148,14 @@ constexpr int kVarCoop = 1 << 16;
 // run-time compiled kernels: the schedule probe's kernel (kVarProbe) and the render kernels that are never
 // launched as the probe (kVarNoProbe) resolve RenderArgs::probe_cost at compile time (offline: at run time)
 constexpr int kVarProbe = 1 << 17, kVarNoProbe = 1 << 18;
+// run-time compiled narrow kernels whose colour records number < 255: 8-bit codes, four levels per LDS word (a
+// d50 Cornell box keeps all 50 levels of every lane in LDS: no colour-stack traffic to HBM)
+constexpr int kVarByte = 1 << 19;
+// run-time compiled kernels whose colour stack lives in LDS entirely (rc_lds_levels >= max_bounces at any
+// residency, rt_capi.cpp): no HBM level code (the deep unwind's batch registers) in the kernel
+constexpr int kVarRcLds = 1 << 20;
 // variant bits the run-time compiled kernels are specialised on
-constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop |
+constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop | kVarByte | kVarRcLds |
                             (15 << kVarMatShift) | (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
@@ -179,11 +192,11 @@ struct RenderArgs {
   uint32_t tiles_x;           // ceil(width / 8)
   uint32_t n_ids;             // 64 * ceil(rows/8) * tiles_x: tile-major pixel ids handed to waves
   // RNG seeding fused into the tile pickup (init_gpu_data's curand_init, raytracing.cu:1591-1606): when a wave
-  // takes a chunk of pixel ids, lane l jumps the state of its pixel's row (rng_rows) over the pixel's column
-  // (binary jump through the nibble tables of P_k = J^(2^k), rng_nib) and leaves it in the wave's slot; the
-  // lanes that take those pixels read their states from there
-  const uint32_t *rng_rows;   // [rows][8] row base states {x0..x4, pad}: subsequence = global row * width
-  const uint32_t *rng_nib;    // kRngNibTableWords per power P_k (xorwow_jump.h kJumpNibbleOffset onwards)
+  // takes a chunk of pixel ids, lane l applies the column table of its pixel's tile column (rng_nib) to the phase
+  // base of its pixel (rng_rows) and leaves the state in the wave's slot; the lanes that take those pixels read
+  // their states from there (xorwow_jump.h xorwow_phase_bases / xorwow_column_tables)
+  const uint32_t *rng_rows;   // [rows][8 columns][8] phase bases {x0..x4, pad}: pixel (lr, c), c < 8
+  const uint32_t *rng_nib;    // [tiles_x][kRngNibTableWords]: nibble table of J^(8 t) for tile column t
   uint32_t rng_d;             // the Weyl word d (the same for every subsequence)
   uint32_t *rng_slot;         // per wave [5][64]: the states of the chunk of pixel ids it took last
   float *out;                 // [n_pixels][3]
@@ -205,6 +218,7 @@ struct RenderArgs {
   uint32_t max_tries;             // rejection tries per round before deferring (0 = unlimited)
   uint32_t accel_nodes, accel_prims, accel_root;   // verified sphere traversal (word offsets, root node)
   uint32_t accel_wide;            // word offset of the 4-wide nodes (kAccel4NodeWords each, root = node 0)
+  uint32_t accel_node_u4;         // uint4 per node of the walked tree (4: BVH2 or quantised 4-wide, 8: 4-wide)
   uint32_t accel_lds_nodes;       // its first nodes (breadth-first: the top levels) staged at LDS word 0
   uint32_t *accel_fallbacks;      // rays the verified traversal handed to the reference walk (diagnostic)
   uint32_t defer_trace;           // verified traversal: the round's walk stops once at most this many

@@ -34,6 +34,7 @@ struct SphereAccel {
   // the same tree 4 wide (accel::collapse_wide, rt_layout.h kAccel4*): root = node 0; wide_stack bounds the
   // ordered walk's stack (up to 3 pushes per level)
   std::vector<uint32_t> wide_words;
+  std::vector<uint32_t> wide_q_words;   // the same nodes quantised (accel::quantize_wide; empty: not quantisable)
   uint32_t wide_depth = 0, wide_stack = 0;
 };
 // false (with a reason) when the world is not an all-sphere BVH/group tree with >= min_spheres spheres

@@ -78,8 +78,9 @@ constexpr int kMixLanes = 32;                   // mixed hot waves (verified mix
 constexpr uint32_t kRcLdsMaxLevels = 256;  // colour-stack levels kept in LDS at most (max_bounces is a u8)
 constexpr uint32_t kSpanWord = 48;          // work words 48..51: the render kernel's span (RenderArgs::span)
 
-// LDS bytes of one colour-stack level for a 256-thread block: 32-bit codes, or 16-bit in narrow kernels
-constexpr size_t rc_level_bytes(bool narrow) { return static_cast<size_t>(rt::kWavesPerBlock) * 64 * (narrow ? 2 : 4); }
+// LDS bytes of one colour-stack level for a 256-thread block: 32-bit codes, 16-bit in narrow kernels, 8-bit in
+// byte kernels (code_bytes 4 / 2 / 1)
+constexpr size_t rc_level_bytes(uint32_t code_bytes) { return static_cast<size_t>(rt::kWavesPerBlock) * 64 * code_bytes; }
 
 // Upper bound on |component| of every ray origin/direction this render can trace (folded traversal
 // precondition, scene_codegen.cpp).  Primary rays: camera centre + lens offset, directions to the
@@ -150,6 +151,7 @@ struct rt_context {
   uint32_t accel_nodes = 0, accel_prims = 0;   // word offsets in the device image
   uint32_t accel_wide = 0;                      // ... of the 4-wide nodes (0: none)
   bool accel_w4 = false;                        // RT_ACCEL_WIDTH=4: the verified walk uses the 4-wide tree
+  bool accel_q = false;                         // ... quantised (RT_ACCEL_QUANT, accel::quantize_wide)
   // top SAH nodes staged in LDS (RT_ACCEL_LDS_NODES): 64 (6 levels, 4 KiB per block) measured best on
   // the 10k scene, 1-3 % over none and over 128 / 256 (profiles/r03_ab_accel_lds_bfs_early*.jsonl)
   uint32_t accel_lds_nodes = 64;
@@ -160,9 +162,11 @@ struct rt_context {
   uint32_t mix_nodes = 0, mix_prims = 0;
   bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
   int static_ok = -1;          // the scene expands within jit_budget (straight-line, stackless traversal); -1 unknown
-  DevBuf scene, jump, rng_rows, rng_slot, rc, work, counters, wave_trace, tile_cost, tile_order;
-  // row base states of the last geometry (xorwow_row_bases), kept on the device: key = seed, W, rows of the shard
+  DevBuf scene, jump, rng_rows, rng_cols, rng_slot, rc, work, counters, wave_trace, tile_cost, tile_order;
+  // seeding tables of the last geometry, kept on the device: the phase bases (xorwow_phase_bases; key = seed, W,
+  // rows of the shard) and the column tables (xorwow_column_tables; key = W)
   uint64_t rows_key[5] = {~0ull, 0, 0, 0, 0};
+  int cols_width = -1;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
   bool counted = false;
@@ -211,7 +215,8 @@ struct rt_context {
   uint64_t samples = 0;
   size_t lds_bytes = 0;
   size_t rc_audit_bytes = 0;      // RT_FLAG_RC_AUDIT: bytes of the HBM colour-stack buffer filled before the render
-  bool rc_audit_narrow = false;   // ... holding 16-bit codes
+  uint32_t rc_audit_code = 4;     // ... holding codes of this many bytes
+  bool rc_no_byte = false;        // RT_RC_BYTE=0: 16-bit codes where 8-bit ones would do (A/B)
   uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
   double jit_ms = 0.0;            // ... and the host time spent obtaining them
@@ -261,6 +266,25 @@ int rt_accel_build_wide(const rt_scene *scene, uint32_t *words, uint64_t cap, ui
   return RT_OK;
 }
 
+int rt_accel_build_quant(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]) {
+  if (!scene || !info) return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  int st = rt::compile_scene(scene, &img);
+  if (st != RT_OK) return st;
+  rt::SphereAccel a;
+  std::string why;
+  if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why) || a.wide_q_words.empty()) return RT_ERR_UNSUPPORTED;
+  info[0] = static_cast<uint32_t>(a.wide_q_words.size() / rt::kAccel4QNodeWords);
+  info[1] = a.wide_depth;
+  info[2] = a.wide_stack;
+  info[3] = static_cast<uint32_t>(a.wide_q_words.size());
+  if (words) {
+    if (cap < a.wide_q_words.size()) return RT_ERR_INVALID_ARG;
+    std::memcpy(words, a.wide_q_words.data(), a.wide_q_words.size() * 4);
+  }
+  return RT_OK;
+}
+
 int rt_mixed_build(const rt_scene *scene, uint32_t info[4]) {
   if (!scene || !info) return RT_ERR_INVALID_ARG;
   rt::SceneImage img;
@@ -302,7 +326,7 @@ void rt_context_destroy(rt_context *c) {
   {
     DeviceGuard g(c->device);
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
-    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_slot.release(); c->rc.release();
+    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->rng_slot.release(); c->rc.release();
     c->work.release(); c->counters.release();
     c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
   }
@@ -346,6 +370,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_TRACE_MIN")) c->trace_min_iters = static_cast<uint32_t>(std::max(1, std::atoi(e)));
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_MIX_PROVE")) c->mix_no_proof = e[0] == '0';
+  if (const char *e = std::getenv("RT_RC_BYTE")) c->rc_no_byte = e[0] == '0';
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     c->accel_lds_set = true;
@@ -372,10 +397,12 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->accel_prims = static_cast<uint32_t>(dev_words.size());
     dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
     c->accel_w4 = rt::accel_width() == 4 && !c->accel.wide_words.empty();
+    c->accel_q = c->accel_w4 && rt::accel_quant() && !c->accel.wide_q_words.empty();
     if (c->accel_w4) {
-      while (dev_words.size() % 4) dev_words.push_back(0);
+      const std::vector<uint32_t> &ww = c->accel_q ? c->accel.wide_q_words : c->accel.wide_words;
+      while (dev_words.size() % 16) dev_words.push_back(0);   // 64-B node lines
       c->accel_wide = static_cast<uint32_t>(dev_words.size());
-      dev_words.insert(dev_words.end(), c->accel.wide_words.begin(), c->accel.wide_words.end());
+      dev_words.insert(dev_words.end(), ww.begin(), ww.end());
     }
   }
   if (c->mixed_ok) {
@@ -482,8 +509,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // colour stack: 16-bit codes in run-time compiled kernels of scenes without noise and texels (and with
   // < 65536 colour records), 32-bit otherwise; the LDS-scene decision is made with the wide size
   const bool narrow_ok = !c->img.has_noise && !c->img.needs_uv && c->img.rec_consts + rt::kRcConsts < 65536u;   // code 0xffff stays unused (RC_AUDIT sentinel)
+  const bool byte_ok = narrow_ok && c->img.rec_consts + rt::kRcConsts < 255u && !c->rc_no_byte;            // 0xff unused likewise
   uint32_t rc_levels = std::min<uint32_t>(mb, c->rc_lds_levels);
-  size_t rc_bytes = rc_levels * rc_level_bytes(false);
+  size_t rc_bytes = rc_levels * rc_level_bytes(4);
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
   // (the mixed walk keeps a macro's SAH stack above the reference walk's entries)
   const uint32_t stack_cap = std::max({c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u,
@@ -502,10 +530,17 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + rc_bytes + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
+  // every colour-stack level of a run-time kernel in LDS at ANY residency (8 blocks/CU), scene staging and per-lane
+  // stacks included: such kernels carry no HBM level code (kVarRcLds).  Set below only when the levels are kept.
+  const uint32_t cb_jit = byte_ok ? 1u : (narrow_ok ? 2u : 4u);
+  const size_t lds_only_need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb_jit) +
+                               (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
+                               (stackless ? 0 : full_stack_bytes) + kLdsReserve;
+  const bool rc_lds_only = c->rc_lds_auto && lds_only_need <= kLdsPerCu / 8;
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
-                        (narrow_ok ? rt::kVarNarrow : 0);
+                        (narrow_ok ? rt::kVarNarrow : 0) | (byte_ok ? rt::kVarByte : 0) | (rc_lds_only ? rt::kVarRcLds : 0);
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
   const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
   if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;
@@ -564,7 +599,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (trav == RT_TRAV_ACCEL) {
     rt::JitKernels jk;
     std::string why;
-    if (rt::jit_accel_kernels(c->img, c->variant | trace_bit, c->accel_w4, &jk, &why)) {
+    if (rt::jit_accel_kernels(c->img, c->variant | trace_bit, c->accel_q ? 2 : (c->accel_w4 ? 1 : 0), &jk, &why)) {
       note_jit(jk);
       jit_fn = c->counted ? jk.render_count : jk.render;
       jit_probe = jk.probe;
@@ -594,23 +629,27 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // itself is not: they take the scene's place at the start of the block's LDS
   uint32_t accel_lds_nodes = 0;
   if (trav == RT_TRAV_ACCEL && !c->lds && c->accel_lds_nodes > 0) {
-    const uint32_t node_words = c->accel_w4 ? rt::kAccel4NodeWords : rt::kAccelNodeWords;
+    const uint32_t node_words = c->accel_q ? rt::kAccel4QNodeWords : (c->accel_w4 ? rt::kAccel4NodeWords : rt::kAccelNodeWords);
     // the same LDS bytes either way by default (64 2-wide nodes = 32 4-wide ones); RT_ACCEL_LDS_NODES counts nodes
     const uint32_t want = c->accel_lds_set ? c->accel_lds_nodes : c->accel_lds_nodes * rt::kAccelNodeWords / node_words;
-    accel_lds_nodes = std::min<uint32_t>(want, static_cast<uint32_t>((c->accel_w4 ? c->accel.wide_words.size()
+    accel_lds_nodes = std::min<uint32_t>(want, static_cast<uint32_t>((c->accel_q ? c->accel.wide_q_words.size() : c->accel_w4 ? c->accel.wide_words.size()
                                                                                   : c->accel.node_words.size()) / node_words));
     // only what the block's LDS budget leaves after the colour-stack levels and the stacks (an explicit
     // RT_RC_LDS_LEVELS may already take most of it): the staging shrinks, the launch never exceeds 160 KiB
-    const bool nw = jit_fn != nullptr && narrow_ok;
-    const size_t used = (nw ? ((rc_levels + 1) & ~1u) : rc_levels) * rc_level_bytes(nw) + stack_bytes + kLdsReserve;
+    const uint32_t cb = jit_fn == nullptr ? 4u : (byte_ok ? 1u : (narrow_ok ? 2u : 4u));
+    const uint32_t per_word = 4u / cb;
+    const size_t used = ((rc_levels + per_word - 1) / per_word * per_word) * rc_level_bytes(cb) + stack_bytes + kLdsReserve;
     const size_t node_bytes = static_cast<size_t>(node_words) * 4;
     const size_t room = used < kLdsPerCu ? (kLdsPerCu - used) / node_bytes : 0;
     accel_lds_nodes = static_cast<uint32_t>(std::min<size_t>(accel_lds_nodes, room));
     scene_lds_words = accel_lds_nodes * node_words;
   }
-  const bool narrow = jit_fn != nullptr && narrow_ok;   // the offline kernels use 32-bit codes
-  const size_t level_bytes = rc_level_bytes(narrow);
-  if (narrow) rc_levels = (rc_levels + 1) & ~1u;        // two levels per LDS word
+  // the offline kernels use 32-bit codes; run-time ones 16-bit (narrow) or 8-bit (byte) where the scene allows
+  const uint32_t code_bytes = jit_fn == nullptr ? 4u : (byte_ok ? 1u : (narrow_ok ? 2u : 4u));
+  const bool lds_only_kernel = jit_fn != nullptr && rc_lds_only;   // its variant carries kVarRcLds (trace_bit)
+  const uint32_t codes_per_word = 4u / code_bytes;
+  const size_t level_bytes = rc_level_bytes(code_bytes);
+  rc_levels = (rc_levels + codes_per_word - 1) / codes_per_word * codes_per_word;   // whole LDS words per lane
   c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + rc_levels * level_bytes + stack_bytes;
   c->used_traversal = trav;
   int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes) : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
@@ -625,12 +664,15 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
       // measured NOT to be co-resident on gfx950 (3 x 53808 B: a third of the blocks started late)
       uint32_t fit = per_block > fixed + kLdsReserve ? static_cast<uint32_t>((per_block - fixed - kLdsReserve) / level_bytes) : 0u;
       uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
-      if (narrow) lv = std::max<uint32_t>(lv & ~1u, rc_levels);   // even (rc_levels already is)
-      if (lv > rc_levels) {
+      lv = std::max<uint32_t>(lv / codes_per_word * codes_per_word, rc_levels);   // whole words (rc_levels already is)
+      // a kernel without HBM levels (kVarRcLds) holds every level: mb rounded up to whole words (the host check
+      // above guarantees they fit at 8 blocks/CU)
+      if (lds_only_kernel) lv = (mb + codes_per_word - 1) / codes_per_word * codes_per_word;
+      if (lv > rc_levels || lds_only_kernel) {
         const size_t lds2 = fixed + lv * level_bytes;
         int per_cu2 = jit_fn ? rt::jit_blocks_per_cu(jit_fn, lds2) : rt::render_blocks_per_cu(c->variant, lds2);
         if (c->blocks_per_cu > 0) per_cu2 = std::min(c->blocks_per_cu, per_cu2);
-        if (per_cu2 >= per_cu) {
+        if (per_cu2 >= per_cu || lds_only_kernel) {
           rc_levels = lv;
           c->lds_bytes = lds2;
         }
@@ -649,30 +691,39 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
 
   const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
   const uint32_t n_ids = 64u * ((static_cast<uint32_t>(p->row_count) + 7) / 8) * tiles_x;
-  // RNG: the row base states of this shard (host, once per geometry: a few ms; the 2M per-pixel jumps run in the
-  // render kernel at tile pickup) and the per-wave slots
+  // RNG: the phase bases of this shard's rows and the column tables (host, once per geometry: a few ms; the
+  // per-pixel jumps — one nibble-table product each — run in the render kernel at tile pickup) and the per-wave
+  // slots
   {
     const uint64_t key[5] = {p->seed, static_cast<uint64_t>(p->width), static_cast<uint64_t>(p->row_offset),
                              static_cast<uint64_t>(p->row_stride), static_cast<uint64_t>(p->row_count)};
     if (std::memcmp(key, c->rows_key, sizeof key) != 0) {
       std::vector<uint32_t> rb;
-      rt::xorwow_row_bases(p->seed, p->width, p->row_offset, p->row_stride, p->row_count, &rb);
+      rt::xorwow_phase_bases(p->seed, p->width, p->row_offset, p->row_stride, p->row_count, &rb);
       if (c->rng_rows.ensure(rb.size() * 4) != hipSuccess ||
           hipMemcpy(c->rng_rows.p, rb.data(), rb.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
         return RT_ERR_HIP;
       std::memcpy(c->rows_key, key, sizeof key);
     }
+    if (c->cols_width != p->width) {
+      std::vector<uint32_t> ct;
+      rt::xorwow_column_tables(p->width, &ct);
+      if (c->rng_cols.ensure(ct.size() * 4) != hipSuccess ||
+          hipMemcpy(c->rng_cols.p, ct.data(), ct.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return RT_ERR_HIP;
+      c->cols_width = p->width;
+    }
   }
   if (c->rng_slot.ensure(static_cast<size_t>(threads / 64) * rt::kRngSlotWords * 4) != hipSuccess) return RT_ERR_HIP;
-  if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;
+  if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;   // (wide codes' size)
   c->used_rc_levels = rc_levels;
   c->rc_audit_bytes = 0;
   // every slot 0xff..: a written code never is — narrow codes are record indices < 65535 (narrow_ok), wide
   // record codes have the sign bit clear, greys are finite with the sign clear, and a texel code's offset is at
   // most pixel_words - 3 < 0x7fffffff (rt_layout.h kRc*)
   if (p->flags & RT_FLAG_RC_AUDIT) {
-    c->rc_audit_bytes = static_cast<size_t>(mb) * threads * (narrow ? 2 : 4);
-    c->rc_audit_narrow = narrow;
+    c->rc_audit_bytes = static_cast<size_t>(mb) * threads * code_bytes;
+    c->rc_audit_code = code_bytes;
     if (hipMemsetAsync(c->rc.p, 0xff, c->rc_audit_bytes, s) != hipSuccess) return RT_ERR_HIP;
   }
 
@@ -692,6 +743,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.accel_root = c->accel.root;
   a.accel_lds_nodes = accel_lds_nodes;
   a.accel_wide = (trav == RT_TRAV_ACCEL && c->accel_w4) ? c->accel_wide : 0u;
+  a.accel_node_u4 = (trav == RT_TRAV_ACCEL && c->accel_w4 && !c->accel_q) ? 8u : 4u;
   a.accel_fallbacks = static_cast<uint32_t *>(c->work.p) + 12;   // zeroed with the work counters
   a.mix_nodes = c->mix_nodes;
   a.mix_prims = c->mix_prims;
@@ -716,7 +768,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.tiles_x = tiles_x;
   a.n_ids = n_ids;
   a.rng_rows = static_cast<const uint32_t *>(c->rng_rows.p);
-  a.rng_nib = static_cast<const uint32_t *>(c->jump.p) + rt::kJumpNibbleOffset;
+  a.rng_nib = static_cast<const uint32_t *>(c->rng_cols.p);
   a.rng_d = seed_base[0];
   a.rng_slot = static_cast<uint32_t *>(c->rng_slot.p);
   a.out = out_dev;
@@ -901,7 +953,7 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   if (c->rc_audit_bytes) {   // RT_FLAG_RC_AUDIT: slots the render wrote
     std::vector<uint8_t> rb(c->rc_audit_bytes);
     if (hipMemcpy(rb.data(), c->rc.p, rb.size(), hipMemcpyDeviceToHost) != hipSuccess) return RT_ERR_HIP;
-    const size_t w = c->rc_audit_narrow ? 2 : 4;
+    const size_t w = c->rc_audit_code;
     uint64_t n = 0;
     for (size_t i = 0; i < rb.size(); i += w) {
       bool untouched = true;
@@ -1004,10 +1056,17 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
   if (rc != RT_OK) return rc;
   while (img.words.size() % 4) img.words.push_back(0);
   const uint32_t mb = static_cast<uint8_t>(max_bounces);
-  const int variant = (img.words.size() <= rt::kLdsSceneMaxWords ? rt::kVarLds : 0) | (img.has_noise ? rt::kVarNoise : 0) |
+  int variant = (img.words.size() <= rt::kLdsSceneMaxWords ? rt::kVarLds : 0) | (img.has_noise ? rt::kVarNoise : 0) |
                       (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img) |
                       (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
-                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0);
+                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0) |
+                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0);
+  {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks)
+    const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
+    const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +
+                        (img.words.size() <= rt::kLdsSceneMaxWords ? img.words.size() * 4 : 4096u) + kLdsReserve;
+    if (traversal == RT_TRAV_STATIC && need <= kLdsPerCu / 8) variant |= rt::kVarRcLds;
+  }
   std::string src;
   if (traversal == RT_TRAV_STATIC) {
     uint32_t v = 0;
@@ -1016,7 +1075,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     rt::SphereAccel a;
     std::string why;
     if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
-    src = rt::jit_accel_source(img, variant, rt::accel_waves(), rt::accel_width() == 4);
+    src = rt::jit_accel_source(img, variant, rt::accel_waves(), rt::accel_width() == 4 ? (rt::accel_quant() ? 2 : 1) : 0);
   } else if (traversal == RT_TRAV_MIXED) {
     rt::MixedAccel m;
     std::string why;
@@ -1079,16 +1138,22 @@ int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int
   return RT_OK;
 }
 
-int rt_rng_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out) {
+int rt_rng_table_states(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out) {
   if (!out || width <= 0 || rows <= 0 || row_offset < 0 || row_stride <= 0) return RT_ERR_INVALID_ARG;
-  std::vector<uint32_t> rb;
-  rt::xorwow_row_bases(seed, width, row_offset, row_stride, rows, &rb);
+  std::vector<uint32_t> pb, ct;
+  rt::xorwow_phase_bases(seed, width, row_offset, row_stride, rows, &pb);
+  rt::xorwow_column_tables(width, &ct);
   uint32_t base[6];
   rt::xorwow_seed_base(seed, base);
-  for (int k = 0; k < rows; ++k) {
-    out[k * 6] = base[0];
-    for (int w = 0; w < 5; ++w) out[k * 6 + 1 + w] = rb[static_cast<size_t>(k) * 8 + w];
-  }
+  for (int lr = 0; lr < rows; ++lr)
+    for (int j = 0; j < width; ++j) {   // the render kernel's pickup: phase base (lr, j & 7), column table j >> 3
+      uint32_t x[5];
+      std::memcpy(x, &pb[(static_cast<size_t>(lr) * 8 + (j & 7)) * 8], sizeof x);
+      rt::xorwow_apply_nib(ct.data() + static_cast<size_t>(j >> 3) * rt::kJumpNibbleWords, x);
+      uint32_t *o = out + (static_cast<size_t>(lr) * width + j) * 6;
+      o[0] = base[0];
+      std::memcpy(o + 1, x, sizeof x);
+    }
   return RT_OK;
 }
 

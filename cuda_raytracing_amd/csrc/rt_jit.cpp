@@ -74,12 +74,14 @@ std::string waves_attr() {
   return "";
 }
 
+std::string waves_attr_n(int waves);
+
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
-                bool *folded) {
+                bool *folded, int waves) {
   std::string trace;
   if (!generate_static_trace(img, max_visits, fold, &trace, visits, folded)) return false;
   const int v = variant & kJitVarMask;
-  const std::string attr = waves_attr();
+  const std::string attr = waves_attr_n(waves);
   *src = "#include \"rt_body.h\"\nnamespace rt {\n" + trace +
          "extern \"C\" __global__ __launch_bounds__(256)" + attr + " void rt_static_render(RenderArgs A) {\n"
          "  render_body<" + std::to_string(v | kVarNoProbe) + ", StaticTrace>(A);\n}\n"
@@ -278,18 +280,6 @@ bool build_module(const std::string &src, const std::string &prefix, JitKernels 
 
 }  // namespace
 
-bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
-  std::string src;
-  uint32_t visits = 0;
-  bool folded = false;
-  if (!jit_source(img, variant, max_visits, fold, &src, &visits, &folded)) {
-    if (why) *why = "scene expansion exceeds " + std::to_string(max_visits) + " node visits";
-    return false;
-  }
-  out->visits = visits;
-  out->folded = folded;
-  return build_module(src, "rt_static", out, why);
-}
 
 int scene_shading_bits(const SceneImage &img) {
   uint32_t mm = 0, tm = 0;
@@ -333,9 +323,10 @@ std::string waves_attr_n(int waves) {
   return waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : waves_attr();
 }
 
-std::string jit_accel_source(const SceneImage &img, int variant, int waves, bool wide) {
+std::string jit_accel_source(const SceneImage &img, int variant, int waves, int wide) {
   const int v = variant & kJitVarMask;
-  const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u, " + (wide ? "true" : "false") + ">";
+  const std::string at = "AccelTraceK<" + std::to_string(scene_kinds(img)) + "u, " + (wide ? "true" : "false") + ", " +
+                         (wide == 2 ? "true" : "false") + ">";
   std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr_n(waves) + " void rt_accel_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarNoProbe) + ", " + at + ">(A);\n}\n";
@@ -367,9 +358,12 @@ std::string jit_mixed_source(const SceneImage &img, int variant, int waves) {
 // One residency step for a few registers: the allocator often lands just above a boundary of the hardware's
 // 16-VGPR granule (the 10k walk at 82 VGPRs = 5 waves/SIMD, 80 would be 6; the mixed walk at 98 = 4, 96 would
 // be 5).  When the render kernel is within kRaiseSlack VGPRs of the next residency, its module is rebuilt
-// with amdgpu_waves_per_eu(that residency) and kept if the kernel then reaches it with no scratch.
-// RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves the first build.
-constexpr int kRaiseSlack = 4;
+// with amdgpu_waves_per_eu(that residency) and kept if the kernel then reaches it with at most kRaiseScratch bytes
+// of scratch per lane (a couple of spilled values outside the hot loops; round 4: the static kernels of scene 0 and
+// the Cornell box land at 81-85 VGPRs, one step above 6 waves).  RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves
+// the first build.
+constexpr int kRaiseSlack = 8;
+constexpr int kRaiseScratch = 16;
 
 int render_vgprs(hipFunction_t fn, int *scratch) {
   int v = 0, sc = 0;
@@ -385,7 +379,7 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out) 
   if (const char *e = std::getenv("RT_JIT_RAISE")) if (e[0] == '0') return;
   int sc0 = 0;
   const int v0 = render_vgprs(out->render, &sc0);
-  if (v0 <= 0 || sc0 != 0) return;
+  if (v0 <= 0 || sc0 < 0 || sc0 > kRaiseScratch) return;
   const int cur = resident_blocks_by_vgprs(v0);
   for (int w = cur + 1; w <= 8; ++w) {
     const int limit = 512 / w / 8 * 8;   // the allocator's budget for w waves (granule 8)
@@ -399,12 +393,34 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out) 
     if (std::getenv("RT_DEBUG"))
       std::fprintf(stderr, "[rt] jit residency raise %s: %d VGPRs (%d/CU) -> waves_per_eu(%d): %d VGPRs, scratch %d B\n",
                    prefix, v0, cur, w, v, sc);
-    if (v > 0 && sc == 0 && resident_blocks_by_vgprs(v) > cur) {
+    if (v > 0 && sc >= 0 && sc <= kRaiseScratch && resident_blocks_by_vgprs(v) > cur) {
       k.ms += out->ms;
       *out = k;
     }
     return;
   }
+}
+
+bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
+  std::string src;
+  uint32_t visits = 0;
+  bool folded = false;
+  if (!jit_source(img, variant, max_visits, fold, &src, &visits, &folded)) {
+    if (why) *why = "scene expansion exceeds " + std::to_string(max_visits) + " node visits";
+    return false;
+  }
+  out->visits = visits;
+  out->folded = folded;
+  if (!build_module(src, "rt_static", out, why)) return false;
+  // one residency step up when the allocator lands just above a boundary (kept only without scratch)
+  raise_residency([&](int w) {
+    std::string s2;
+    uint32_t v2 = 0;
+    bool f2 = false;
+    jit_source(img, variant, max_visits, fold, &s2, &v2, &f2, w);
+    return s2;
+  }, "rt_static", out);
+  return true;
 }
 
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
@@ -431,13 +447,19 @@ int accel_width() {
   return 2;
 }
 
+// The 4-wide tree quantised (accel::quantize_wide, 64-B nodes) or as float planes (128-B nodes): RT_ACCEL_QUANT=0/1
+bool accel_quant() {
+  if (const char *e = std::getenv("RT_ACCEL_QUANT")) return e[0] != '0';
+  return true;
+}
+
 // The default 6-wave request is measured on the plain 10k walk, whose 80-VGPR build spills ~17 VGPRs outside
 // the node loop (44 B per lane).  Variants that need far more registers (noise, image u,v, deep bounces:
 // 125-149 VGPRs) would spill inside their hot loops; a default-request build with more scratch than this is
 // replaced by the allocator's own build (+ the residency raise).  An explicit RT_ACCEL_WAVES is kept as built.
 constexpr int kAccelWavesScratchMax = 96;
 
-bool jit_accel_kernels(const SceneImage &img, int variant, bool wide, JitKernels *out, std::string *why) {
+bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
   int w = accel_waves();

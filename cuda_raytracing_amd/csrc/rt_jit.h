@@ -27,7 +27,7 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
 
 // Full hipRTC source of the StaticTrace kernels for `variant` (no device needed).
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
-                bool *folded = nullptr);
+                bool *folded = nullptr, int waves = 0);   // waves > 0: amdgpu_waves_per_eu (0: RT_JIT_WAVES or none)
 // Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
 
@@ -37,9 +37,10 @@ bool jit_lane_kernels(const SceneImage &img, int variant, JitKernels *out, std::
 std::string jit_lane_source(const SceneImage &img, int variant);
 // Verified sphere traversal kernels (AccelTraceK over the scene's node kinds for the fallback walk); wide: the
 // 4-wide tree (SphereAccel::wide_words)
-bool jit_accel_kernels(const SceneImage &img, int variant, bool wide, JitKernels *out, std::string *why);
-std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0, bool wide = false);   // waves > 0: amdgpu_waves_per_eu
+bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why);   // wide: 0 BVH2, 1 4-wide, 2 quantised 4-wide
+std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0, int wide = 0);   // waves > 0: amdgpu_waves_per_eu
 int accel_width();   // 2 or 4 (RT_ACCEL_WIDTH)
+bool accel_quant();  // the 4-wide tree quantised (RT_ACCEL_QUANT, default on)
 int accel_waves();   // the verified sphere walk's waves per SIMD request (6; RT_ACCEL_WAVES, 0 = allocator's choice)
 // verified mixed-world traversal kernels (MixedTraceK over the scene's node kinds)
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);

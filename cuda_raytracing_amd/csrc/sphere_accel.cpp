@@ -118,6 +118,7 @@ bool build_sphere_accel(const SceneImage &img, uint32_t min_spheres, SphereAccel
   out->wide_words = accel::collapse_wide(bd.nodes, root, &out->wide_depth);
   out->wide_stack = 3 * out->wide_depth + 1;
   if (out->wide_words.size() / kAccel4NodeWords >= 65536) out->wide_words.clear();   // u16 stack entries
+  if (!out->wide_words.empty()) accel::quantize_wide(out->wide_words, &out->wide_q_words);
   out->spheres = static_cast<uint32_t>(bd.order.size());
   out->node_words = bd.nodes;
   out->prim_words.assign(static_cast<size_t>(bd.order.size()) * kAccelPrimWords, 0);

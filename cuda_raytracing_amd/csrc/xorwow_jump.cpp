@@ -88,7 +88,11 @@ void power_matrix(const std::vector<uint32_t> &T, uint64_t n, Mat &m) {
 }  // namespace
 
 void xorwow_jump_nib(const uint32_t *tables, int k, uint32_t x[5]) {
-  const uint32_t *lo = tables + kJumpNibbleOffset + static_cast<size_t>(k) * kJumpNibbleWords;
+  xorwow_apply_nib(tables + kJumpNibbleOffset + static_cast<size_t>(k) * kJumpNibbleWords, x);
+}
+
+void xorwow_apply_nib(const uint32_t *tab, uint32_t x[5]) {
+  const uint32_t *lo = tab;
   const uint32_t *hi = lo + kJumpNibbles * 16 * 4;
   uint32_t r[5] = {0, 0, 0, 0, 0};
   for (int c = 0; c < kJumpNibbles; ++c) {
@@ -111,6 +115,48 @@ void xorwow_row_bases(uint64_t seed, int width, int row_offset, int row_stride, 
   for (int lr = 0; lr < rows; ++lr) {
     std::memcpy(&(*out)[static_cast<size_t>(lr) * 8], x, sizeof x);
     if (lr + 1 < rows) apply(m, x);
+  }
+}
+
+void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out) {
+  std::vector<uint32_t> rb;
+  xorwow_row_bases(seed, width, row_offset, row_stride, rows, &rb);
+  out->assign(static_cast<size_t>(rows > 0 ? rows : 0) * 64, 0u);
+  const std::vector<uint32_t> &T = xorwow_jump_tables();
+  for (int lr = 0; lr < rows; ++lr) {
+    uint32_t x[5];
+    std::memcpy(x, &rb[static_cast<size_t>(lr) * 8], sizeof x);
+    for (int c = 0; c < 8; ++c) {
+      std::memcpy(&(*out)[(static_cast<size_t>(lr) * 8 + c) * 8], x, sizeof x);
+      if (c + 1 < width) xorwow_jump_nib(T.data(), 0, x);   // the next column: subsequence + 1 = P_0
+    }
+  }
+}
+
+void xorwow_column_tables(int width, std::vector<uint32_t> *out) {
+  const int tiles = width > 0 ? (width + 7) / 8 : 0;
+  out->assign(static_cast<size_t>(tiles) * kJumpNibbleWords, 0u);
+  const std::vector<uint32_t> &T = xorwow_jump_tables();
+  // M_t = J^(8 t), rows[b] = image of e_b: M_0 = I, M_t = P_3 M_{t-1} (column by column through P_3's table)
+  Mat m;
+  for (int b = 0; b < 160; ++b) {
+    std::memset(m.r[b], 0, sizeof m.r[b]);
+    m.r[b][b >> 5] = 1u << (b & 31);
+  }
+  for (int t = 0; t < tiles; ++t) {
+    if (t > 0)
+      for (int b = 0; b < 160; ++b) xorwow_jump_nib(T.data(), 3, m.r[b]);
+    uint32_t *lo = out->data() + static_cast<size_t>(t) * kJumpNibbleWords;
+    uint32_t *hi = lo + kJumpNibbles * 16 * 4;
+    for (int c = 0; c < kJumpNibbles; ++c)
+      for (int v = 0; v < 16; ++v) {
+        uint32_t r[5] = {0, 0, 0, 0, 0};
+        for (int i = 0; i < 4; ++i)
+          if ((v >> i) & 1)
+            for (int w = 0; w < 5; ++w) r[w] ^= m.r[4 * c + i][w];
+        for (int w = 0; w < 4; ++w) lo[(c * 16 + v) * 4 + w] = r[w];
+        hi[c * 16 + v] = r[4];
+      }
   }
 }
 

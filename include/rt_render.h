@@ -235,16 +235,21 @@ int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_
  * needed): info = {wide nodes, depth, stack bound of the ordered walk, node words}; words (if non-null, cap
  * words) receives the node words.  RT_ERR_UNSUPPORTED when the world is not eligible. */
 int rt_accel_build_wide(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
+/* The 4-wide tree quantised (the verified walk's default 4-wide form, RT_ACCEL_QUANT; device/rt_layout.h kAccel4Q*,
+ * one 64-B line per node; no device needed): info and words as rt_accel_build_wide's, same node numbering.
+ * RT_ERR_UNSUPPORTED when the world is not eligible or its boxes exceed the quantiser's exponent range. */
+int rt_accel_build_quant(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
 /* The per-pixel XORWOW states rt_render seeds on the device (init_gpu_data's curand_init,
  * raytracing.cu:1591-1606, subsequence = global pixel index), for rows row_offset + k*row_stride,
  * k < rows, of a width-wide frame: out_states (host) receives [6][rows*width] words {d, x0..x4}.
  * Diagnostics/tests: the render path seeds into device memory and never copies the states back. */
 int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out_states);
-/* The row base states the render seeds its pixels from (no device needed; tests): for rows row_offset +
- * k*row_stride, k < rows, of a width-wide frame, out (rows*6 words) receives {d, x0..x4} of the state of the
- * row's first pixel (subsequence = global row * width).  The render kernel jumps each pixel's state from its
- * row's over the column index at tile pickup (RenderArgs::rng_rows). */
-int rt_rng_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out);
+/* The per-pixel states as the render kernel derives them at tile pickup, computed on the host from the same
+ * tables (no device needed; tests): phase base (row, column & 7) — the row's first state jumped over its first
+ * columns — times the nibble table of J^(8 * (column >> 3)).  For rows row_offset + k*row_stride, k < rows, of
+ * a width-wide frame, out (rows*width*6 words, pixel-major) receives {d, x0..x4}; equal to rt_seed_states's
+ * states of the same pixels. */
+int rt_rng_table_states(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out);
 /* Last fallback reason of a context (why RT_TRAV_STATIC was not used); "" if none. */
 const char *rt_context_note(const rt_context *ctx);
 

@@ -163,3 +163,37 @@ def test_wide_tree_is_the_same_tree_four_wide(idx):
     assert {k: tuple(np.array(v, np.uint32)) for k, v in leaves2.items()} == leaves4
     assert kids == list(range(1, len(wn)))   # breadth-first
     assert winfo["stack"] == 3 * winfo["depth"] + 1 and winfo["depth"] <= info["depth"]
+
+
+@pytest.mark.parametrize("idx", [2, rt.RT_SCENE_RANDOM_10K])
+def test_quantised_wide_tree_contains_the_float_boxes(idx):
+    # accel::quantize_wide (rt_layout.h kAccel4Q*): same refs and numbering as the float 4-wide nodes; the valid
+    # mask marks the non-empty slots; every decoded box (origin + q * 2^e, exact in float64) contains its float
+    # box widened by 2^-20 of the node's largest |plane| on the axis (the kernel's evaluation rounding), and stays
+    # within two steps of it (the quantisation is outward rounding, not a looser box)
+    w, _ = rt.build_scene(idx)
+    _, wn = rt.accel_build_wide(w.scene())
+    qi, qn = rt.accel_build_wide(w.scene(), quant=True)
+    wn = wn.reshape(-1, 32)
+    qn = qn.reshape(-1, 16)
+    assert len(qn) == len(wn) == qi["nodes"]
+    for fw, q in zip(wn, qn):
+        assert [int(x) for x in q[10:14]] == [int(x) for x in fw[24:28]]
+        meta = int(q[3])
+        org = f(q[0:3]).astype(np.float64)
+        for c in range(4):
+            box = f(np.array([fw[4 * k + c] for k in range(6)], np.uint32)).astype(np.float64)
+            empty = np.isinf(box[0]) and box[0] > 0
+            assert bool(meta >> (24 + c) & 1) == (not empty)
+            if empty:
+                continue
+            for a in range(3):
+                lo_all = [f(np.array([fw[8 * a + cc]], np.uint32))[0] for cc in range(4) if meta >> (24 + cc) & 1]
+                hi_all = [f(np.array([fw[8 * a + 4 + cc]], np.uint32))[0] for cc in range(4) if meta >> (24 + cc) & 1]
+                ep = max(abs(min(lo_all)), abs(max(hi_all))) * 2.0 ** -20
+                step = 2.0 ** (((meta >> (8 * a)) & 0xff) - 127)
+                ql = (int(q[4 + 2 * a]) >> (8 * c)) & 0xff
+                qh = (int(q[5 + 2 * a]) >> (8 * c)) & 0xff
+                lo, hi = org[a] + ql * step, org[a] + qh * step
+                assert lo <= box[2 * a] - ep and hi >= box[2 * a + 1] + ep, (a, c)
+                assert lo > box[2 * a] - ep - 2 * step and hi < box[2 * a + 1] + ep + 2 * step, (a, c)

@@ -736,7 +736,8 @@ def test_colour_stack_hbm_levels_vs_oracle(idx, W, H, spp, levels, monkeypatch):
     monkeypatch.setenv("RT_RC_LDS_LEVELS", levels)
     w, s = rt.build_scene(idx)
     forces = SPILL_FORCES + ([rt.RT_FLAG_FORCE_ACCEL] if idx == 20 else [])
-    _spill_check(w, s, W, H, spp, 50, forces, {int(levels), int(levels) + 1})
+    L = int(levels)   # 16-bit codes round the LDS levels up to even, 8-bit codes (kVarByte) to a multiple of 4
+    _spill_check(w, s, W, H, spp, 50, forces, {L, L + 1, (L + 3) // 4 * 4})
 
 
 @pytest.mark.parametrize("levels", ["4", "5"])
@@ -747,7 +748,8 @@ def test_colour_stack_hbm_levels_random_worlds(seed, levels, monkeypatch):
     # a closed diffuse room around the camera and the random objects: paths end only at lights, at
     # absorbing metal bounces or at depth 50, so many are deeper than the LDS levels
     w.box((-20.0, -20.0, -20.0), (20.0, 20.0, 20.0), w.lambert((0.8, 0.75, 0.7)))
-    _spill_check(w, s, 48, 27, 8, 50, SPILL_FORCES, {int(levels), int(levels) + 1})
+    L = int(levels)
+    _spill_check(w, s, 48, 27, 8, 50, SPILL_FORCES, {L, L + 1, (L + 3) // 4 * 4})
 
 
 @pytest.mark.parametrize("b", [16, 17])
@@ -1002,9 +1004,12 @@ def test_kernel_span_within_event_window():
 
 
 # ---- the verified sphere walk over the 4-wide tree (RT_ACCEL_WIDTH=4, accel::collapse_wide) ----
-@pytest.mark.parametrize("idx,W,H,spp", [(2, 64, 36, 4), (20, 160, 90, 6), (20, 480, 270, 4)])
-def test_wide_verified_sphere_traversal_matches_oracle(idx, W, H, spp, monkeypatch):
+# (quantised 64-B nodes by default, accel::quantize_wide; RT_ACCEL_QUANT=0: the float 128-B nodes)
+@pytest.mark.parametrize("idx,W,H,spp,quant", [(2, 64, 36, 4, "1"), (20, 160, 90, 6, "1"), (20, 480, 270, 4, "1"),
+                                               (2, 64, 36, 4, "0"), (20, 160, 90, 6, "0")])
+def test_wide_verified_sphere_traversal_matches_oracle(idx, W, H, spp, quant, monkeypatch):
     monkeypatch.setenv("RT_ACCEL_WIDTH", "4")
+    monkeypatch.setenv("RT_ACCEL_QUANT", quant)
     w, s = rt.build_scene(idx)
     cam, W, H = rt.camera_from_settings(s, W, H)
     p = rt.make_params(s, W, H, spp=spp, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL)
@@ -1025,9 +1030,10 @@ def test_wide_verified_sphere_traversal_matches_oracle(idx, W, H, spp, monkeypat
     assert 0 < a["exec_node"] and 0 < a["exec_prim"]
 
 
-@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4, 5])
-def test_wide_random_sphere_worlds_verified_walk(seed, monkeypatch):
+@pytest.mark.parametrize("seed,quant", [(0, "1"), (1, "1"), (2, "1"), (3, "1"), (4, "1"), (5, "1"), (0, "0"), (3, "0")])
+def test_wide_random_sphere_worlds_verified_walk(seed, quant, monkeypatch):
     monkeypatch.setenv("RT_ACCEL_WIDTH", "4")
+    monkeypatch.setenv("RT_ACCEL_QUANT", quant)
     w, s = _random_sphere_world(seed)
     cam, W, H = rt.camera_from_settings(s, 64, 36)
     p = rt.make_params(s, W, H, spp=4, bounces=12)
@@ -1037,3 +1043,18 @@ def test_wide_random_sphere_worlds_verified_walk(seed, monkeypatch):
     fb, st = gpu(w.scene(), cam, p)
     assert st.traversal == rt.RT_TRAV_ACCEL
     assert np.array_equal(bits(fb), bits(ref))
+
+
+@pytest.mark.parametrize("byte", ["1", "0"])
+def test_byte_colour_codes_all_levels_in_lds(byte, monkeypatch):
+    # Cornell box (few colour records): 8-bit codes keep all 50 levels in LDS by default (RT_RC_BYTE=0: 16-bit codes,
+    # fewer LDS levels); both bit-exact vs the oracle
+    monkeypatch.setenv("RT_RC_BYTE", byte)
+    w, s = rt.build_scene(1)
+    cam, W, H = rt.camera_from_settings(s, 40, 40)
+    p = rt.make_params(s, W, H, spp=4, bounces=50, flags=rt.RT_FLAG_RC_AUDIT)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    fb, st = gpu(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+    if byte == "1":
+        assert st.rc_lds_levels >= 50 and st.rc_hbm_slots == 0, (st.rc_lds_levels, st.rc_hbm_slots)

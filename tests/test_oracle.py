@@ -189,25 +189,28 @@ def test_image_texture_scene_renders():
     assert len(np.unique(fb.reshape(-1, 3), axis=0)) > 50
 
 
-@pytest.mark.parametrize("width,row_offset,row_stride,rows", [(1920, 0, 1, 40), (37, 3, 5, 17), (3840, 7, 8, 9), (1, 0, 1, 5)])
-def test_rng_row_bases_match_the_oracles_seeding(width, row_offset, row_stride, rows):
-    # the host half of the render kernel's fused seeding (rt_rng_row_bases, xorwow_row_bases: the state of each
-    # row's first pixel by the 2^67-step jump powers): its first draws equal the oracle's rocrand_init draws for
-    # subsequence (global row) * width (the device half, the jump over the column, is checked by every GPU frame)
+@pytest.mark.parametrize("width,row_offset,row_stride,rows", [(1920, 0, 1, 3), (37, 3, 5, 17), (3840, 7, 8, 2), (1, 0, 1, 5),
+                                                                 (13, 0, 1, 2)])
+def test_rng_table_states_match_the_oracles_seeding(width, row_offset, row_stride, rows):
+    # the render kernel's fused seeding, restated on the host (rt_rng_table_states: phase base of (row, column & 7)
+    # times the column table of J^(8 * (column >> 3)), the tables the kernel reads): every pixel's first draws
+    # equal the oracle's rocrand_init draws for subsequence (global row) * width + column
     import ctypes as C
     from cuda_raytracing_amd import _abi
-    st = np.zeros((rows, 6), np.uint32)
-    assert _abi.hip_lib().rt_rng_row_bases(1234, width, row_offset, row_stride, rows, st.ctypes.data_as(C.c_void_p)) == 0
+    st = np.zeros((rows * width, 6), np.uint32)
+    assert _abi.hip_lib().rt_rng_table_states(1234, width, row_offset, row_stride, rows, st.ctypes.data_as(C.c_void_p)) == 0
     L = _abi.oracle_lib()
+    cols = sorted(set(range(min(width, 11))) | {width - 1, width // 2, max(0, width - 9)})
     for k in range(rows):
-        d, x0, x1, x2, x3, x4 = (int(v) for v in st[k])
-        got = []
-        for _ in range(8):
-            t = (x0 ^ (x0 >> 2)) & 0xffffffff
-            x0, x1, x2, x3 = x1, x2, x3, x4
-            x4 = (x4 ^ (x4 << 4) ^ t ^ (t << 1)) & 0xffffffff
-            d = (d + 362437) & 0xffffffff
-            got.append(np.float32(np.float32((d + x4) & 0xffffffff) * np.float32(2.0 ** -32) + np.float32(2.0 ** -32)))
-        ref = np.zeros(8, np.float32)
-        L.rt_oracle_uniforms(1234, (row_offset + k * row_stride) * width, ref.ctypes.data_as(C.c_void_p), 8)
-        assert np.array_equal(np.array(got, np.float32), ref), k
+        for j in cols:
+            d, x0, x1, x2, x3, x4 = (int(v) for v in st[k * width + j])
+            got = []
+            for _ in range(4):
+                t = (x0 ^ (x0 >> 2)) & 0xffffffff
+                x0, x1, x2, x3 = x1, x2, x3, x4
+                x4 = (x4 ^ (x4 << 4) ^ t ^ (t << 1)) & 0xffffffff
+                d = (d + 362437) & 0xffffffff
+                got.append(np.float32(np.float32((d + x4) & 0xffffffff) * np.float32(2.0 ** -32) + np.float32(2.0 ** -32)))
+            ref = np.zeros(4, np.float32)
+            L.rt_oracle_uniforms(1234, (row_offset + k * row_stride) * width + j, ref.ctypes.data_as(C.c_void_p), 4)
+            assert np.array_equal(np.array(got, np.float32), ref), (k, j)
