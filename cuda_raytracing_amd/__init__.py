@@ -367,6 +367,23 @@ def accel_build_wide(scene: Scene, quant: bool = False):
     return {"nodes": info[0], "depth": info[1], "stack": info[2]}, buf
 
 
+def prim_lists(scene: Scene, camera: Camera, params: Params, cap: int = 128):
+    """The verified sphere walk's primary-ray candidate lists of a frame, built on the host (no device needed):
+    (counts [tiles] uint32 with 0xffffffff = no list, lists [tiles, cap, 2] uint32 {SAH prim index, axial bound
+    bits}, rho), or None when the world is not eligible."""
+    L = _abi.hip_lib()
+    tiles = ((params.width + 7) // 8) * ((params.row_count + 7) // 8)
+    counts = np.zeros(tiles, np.uint32)
+    lists = np.zeros((tiles, cap, 2), np.uint32)
+    rho = C.c_float()
+    rc = L.rt_prim_lists(C.byref(scene), C.byref(camera), C.byref(params), cap, counts.ctypes.data_as(C.c_void_p),
+                         lists.ctypes.data_as(C.c_void_p), C.byref(rho))
+    if rc == _abi.RT_ERR_UNSUPPORTED:
+        return None
+    _check(rc, "rt_prim_lists")
+    return counts, lists, rho.value
+
+
 def mixed_build(scene: Scene):
     """Macro roots of the verified mixed-world traversal (no device needed): dict, or None when no
     transform-free subtree qualifies."""

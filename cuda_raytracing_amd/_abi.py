@@ -179,7 +179,7 @@ HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_contex
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
                "rt_seed_states", "rt_kernel_source", "rt_mixed_build", "rt_multi_create", "rt_multi_render",
                "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map", "rt_accel_build_wide", "rt_rng_table_states",
-               "rt_accel_build_quant"]
+               "rt_accel_build_quant", "rt_prim_lists"]
 
 
 def _bind_single_hip_runtime():
@@ -231,6 +231,8 @@ def hip_lib():
         _sig(L.rt_mixed_build, C.c_int, C.POINTER(Scene), C.POINTER(C.c_uint32))
         opt("rt_accel_build_wide", C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
         opt("rt_accel_build_quant", C.c_int, C.POINTER(Scene), P, C.c_uint64, C.POINTER(C.c_uint32))
+        opt("rt_prim_lists", C.c_int, C.POINTER(Scene), C.POINTER(Camera), C.POINTER(Params), C.c_uint32, P, P,
+            C.POINTER(C.c_float))
         opt("rt_rng_table_states", C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_seed_states, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_kernel_source, C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.c_char_p, C.c_uint64)

@@ -960,6 +960,30 @@ struct AccelTraceK {
       // walk, the round's walk ends once few lanes remain (A.defer_trace, after A.trace_min_iters
       // steps); those lanes keep node, stack and best hit and resume next round, skipping shading
       // meanwhile.  A walk's steps and order are unchanged, so the record is the same.
+      // A camera ray of a tile with a candidate list (RenderArgs::prim_lists, T.atie = tile + 1): the list's spheres
+      // in ascending order of their axial lower bound instead of the walk — any set of spheres holding every one
+      // the ray could accept gives the same record ((1) above), and a sphere whose lower bound lies beyond the
+      // ray's axial reach below tmax (|o - centre| + tmax |d|, rounded up) cannot yield a root below tmax, nor
+      // can any later one; the reach proof and the fallback below apply unchanged
+      if (!resume && T.atie != 0u) {
+        const uint32_t tile = T.atie - 1u;
+        const uint32_t n = A.prim_counts[tile];
+        if (n <= A.prim_cap) {
+          walking = false;
+          const float dl = sqrtf(dot(r.d, r.d));
+          const uint2 *L = reinterpret_cast<const uint2 *>(A.prim_lists) + static_cast<size_t>(tile) * A.prim_cap;
+          for (uint32_t k = 0; k < n; ++k) {
+            const uint2 e = L[k];
+            if (__uint_as_float(e.y) > __builtin_fmaf(T.tmax, dl, A.prim_rho) * 1.0000010f) break;
+            if (COUNT) vc.xp++;
+            const uint32_t pr = e.x;
+            const uint4 p0 = P[pr * 4], pw1 = P[pr * 4 + 1], pw2 = P[pr * 4 + 2];
+            if (sphere_hit_tie<UV, true, false>(T, r, h, pw2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)),
+                                                mk(asf(p0.w), asf(pw1.x), asf(pw1.y)), asf(pw1.z), asf(pw1.w), sa2, sra2, tie))
+              best = pr;
+          }
+        }
+      }
       const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(walking)));
       // the top of the tree from LDS (A.accel_lds_nodes breadth-first nodes), the rest from HBM / L2
       // (two explicit loads rather than one generic pointer: flat loads would wait on both counters)
@@ -1163,6 +1187,7 @@ struct AccelTraceK {
   // rejection sampling rebuilds the same record from the same words).  T.abest: a SAH prim, or | kBestRecord a
   // reference record (the fallback walk's hit).
   static constexpr bool kLazyHit = true;
+  static constexpr bool kPrimLists = true;   // camera rays may take their tile's candidate list (T.atie)
   template <bool LDS, bool UV>
   __device__ __forceinline__ static void materialize(const Mem<LDS> &S, const RenderArgs &A, const Trav &T, const Ray &r,
                                                      Hit &h) {
@@ -1193,6 +1218,8 @@ struct AccelTraceK {
 // Traces whose hit record is rebuilt at shading time (kLazyHit) — detected without <type_traits> (hipRTC)
 template <class TR> __device__ constexpr auto lazy_hit(int) -> decltype(TR::kLazyHit, bool()) { return TR::kLazyHit; }
 template <class TR> __device__ constexpr bool lazy_hit(long) { return false; }
+template <class TR> __device__ constexpr auto prim_lists(int) -> decltype(TR::kPrimLists, bool()) { return TR::kPrimLists; }
+template <class TR> __device__ constexpr bool prim_lists(long) { return false; }
 
 // ---------------------------------------------------------------------------------------------
 // traversal policy 5: verified traversal of mixed worlds (mixed_accel.cpp)
@@ -1823,7 +1850,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   bool busy = false;                      // lane owns a pixel
   bool hot = false;                       // the pixel is one of the first A.prio_ids handed out
   uint32_t prio_now = 0;                  // wave-uniform: the s_setprio level in force
-  int32_t pix = 0, sample = 0;
+  uint32_t pxy = 0;                       // the pixel: local row << 16 | column (rt_capi.cpp: both < 65536)
+  int32_t sample = 0;
   uint32_t depth = 0;                     // bounces of the current path (max_bounces, :1336)
   uint32_t rsp = 0;                       // colour-stack levels pushed (dielectric bounces push none)
   Rng rng{0, 0, 0, 0, 0, 0};
@@ -1858,10 +1886,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   uint32_t pending = 0;   // 1: the lane's rejection sampling continues next round (A.max_tries)
   float random_test = 0.0f;
   const uint32_t try_cap = A.max_tries ? A.max_tries : 0xffffffffu;
-  // the pixel's viewport point (:1565-1567), recomputed per sample from pix (a few ops; three fewer registers
-  // carried across the trace)
+  // the pixel's viewport point (:1565-1567), recomputed per sample from pxy (a few ops and no division; three
+  // fewer registers carried across the trace)
   auto pixel_point = [&]() -> f3 {
-    const int32_t lr = pix / A.width, j = pix - lr * A.width;
+    const int32_t lr = static_cast<int32_t>(pxy >> 16), j = static_cast<int32_t>(pxy & 0xffffu);
     const int32_t i = A.row_offset + lr * A.row_stride;
     return add(mk(A.p00[0], A.p00[1], A.p00[2]),
              add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
@@ -2005,14 +2033,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
         const uint32_t lr = ty * 8 + (k >> 3), j = tx * 8 + (k & 7u);
         if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
-          pix = static_cast<int32_t>(lr * A.width + j);
+          pxy = (lr << 16) | j;
           need = false;
           busy = true;
           hot = id < A.prio_ids;
           if (probe) {                      // throwaway stream: the real ones are not consumed
             probe_tile = tile;
             probe_rounds = 0;
-            uint32_t hsh = static_cast<uint32_t>(pix) * 0x9E3779B9u + 0x7F4A7C15u + salt * 0x632BE5ABu;
+            uint32_t hsh = (lr * static_cast<uint32_t>(A.width) + j) * 0x9E3779B9u + 0x7F4A7C15u + salt * 0x632BE5ABu;
             hsh ^= hsh >> 16; hsh *= 0x85EBCA6Bu; hsh ^= hsh >> 13; hsh *= 0xC2B2AE35u; hsh ^= hsh >> 16;
             rng.d = hsh; rng.x0 = hsh ^ 0x2c7f967fu; rng.x1 = hsh * 3u + 1u; rng.x2 = ~hsh;
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
@@ -2073,6 +2101,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 
     // ---- trace one path segment per busy lane (hit(), :1340) ----
     const bool tracing = busy && !pending;   // a lane still resuming its rejection keeps its hit
+    if constexpr (prim_lists<Trace>(0)) {
+      // a camera ray (no bounce yet, no paused walk) of a shard with candidate lists: its tile's list
+      T.atie = 0u;
+      if (A.prim_lists && tracing && depth == 0u && !T.active) {
+        T.atie = (pxy >> 19) * A.tiles_x + ((pxy & 0xffffu) >> 3) + 1u;
+      }
+    }
     Trace::template run<LDS, COUNT, UV>(S, A, tracing, __ballot(tracing), lane, stk, T, ray, h, vc);
     if (T.active) continue;                   // walk paused (verified traversal): resumes next round
     if constexpr (lazy_hit<Trace>(0)) Trace::template materialize<LDS, UV>(S, A, T, ray, h);
@@ -2299,13 +2334,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         probe_end = true;   // its rounds are added to the tile's cost at the top of the next round
         busy = false;
       } else if (sample == A.spp) {
-        float *o = A.out + 3 * static_cast<size_t>(pix);
+        const size_t pix = static_cast<size_t>(pxy >> 16) * static_cast<uint32_t>(A.width) + (pxy & 0xffffu);
+        float *o = A.out + 3 * pix;
         const f3 c = mk(sum.x * A.sample_scale, sum.y * A.sample_scale, sum.z * A.sample_scale);
         o[0] = c.x;
         o[1] = c.y;
         o[2] = c.z;
         if (A.out8) {   // pixels_to_ppm's bytes of the same floats (:1391-1395, 1419-1431), fused
-          uint8_t *b = A.out8 + 3 * static_cast<size_t>(pix);
+          uint8_t *b = A.out8 + 3 * pix;
           b[0] = ppm_byte(c.x);
           b[1] = ppm_byte(c.y);
           b[2] = ppm_byte(c.z);

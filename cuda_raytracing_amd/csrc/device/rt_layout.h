@@ -221,6 +221,13 @@ struct RenderArgs {
   uint32_t accel_node_u4;         // uint4 per node of the walked tree (4: BVH2 or quantised 4-wide, 8: 4-wide)
   uint32_t accel_lds_nodes;       // its first nodes (breadth-first: the top levels) staged at LDS word 0
   uint32_t *accel_fallbacks;      // rays the verified traversal handed to the reference walk (diagnostic)
+  // Primary-ray candidate lists (verified sphere walk; prim_list_kernel): per 8x8 tile of the shard, the spheres
+  // whose padded ball meets the cone that holds every camera ray of the tile, ascending by a lower bound of
+  // their distance along the cone axis; a camera ray tests them in that order instead of walking the tree
+  const uint32_t *prim_lists;     // [tiles][prim_cap][2] {sphere index, axial lower bound (float bits)}; null = off
+  const uint32_t *prim_counts;    // [tiles] entries; > prim_cap: no list (overflow), the ray walks the tree
+  uint32_t prim_cap;
+  float prim_rho;                 // bound on |ray origin - camera centre| (defocus disc, rounding included)
   uint32_t defer_trace;           // verified traversal: the round's walk stops once at most this many
   uint32_t trace_min_iters;       // lanes (and <= 1/4 of the starters) still walk, after this many steps
   uint32_t prio_ids;              // pixels among the first prio_ids handed out (the costliest tiles of

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <string>
 #include <vector>
@@ -54,6 +55,8 @@ int params_check(const rt_params *p) {
     return RT_ERR_INVALID_ARG;
   if (static_cast<uint64_t>(p->row_count) * static_cast<uint64_t>(p->width) > 0x7fffffffull) return RT_ERR_INVALID_ARG;
   if (static_cast<uint64_t>(p->height) * static_cast<uint64_t>(p->width) >= (1ull << 40)) return RT_ERR_INVALID_ARG;
+  // the render kernel holds a lane's pixel as local row << 16 | column
+  if (p->width > 65535 || p->row_count > 65535) return RT_ERR_UNSUPPORTED;
   return RT_OK;
 }
 
@@ -156,13 +159,17 @@ struct rt_context {
   // the 10k scene, 1-3 % over none and over 128 / 256 (profiles/r03_ab_accel_lds_bfs_early*.jsonl)
   uint32_t accel_lds_nodes = 64;
   bool accel_lds_set = false;   // RT_ACCEL_LDS_NODES given (nodes of the tree in use)
+  // primary-ray candidate lists of the verified sphere walk (device/prim_lists.h; RT_ACCEL_PRIM=0: off)
+  bool prim_on = true;
+  uint32_t prim_cap = 128;      // entries per tile (RT_PRIM_CAP); a fuller tile's rays walk the tree
+  double accel_half_motion = 0;   // max |motion| / 2 over the SAH tree's spheres
   // verified mixed-world traversal (RT_TRAV_MIXED): macro roots marked in the image, SAH words appended
   rt::MixedAccel mixed;
   bool mixed_ok = false;
   uint32_t mix_nodes = 0, mix_prims = 0;
   bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
   int static_ok = -1;          // the scene expands within jit_budget (straight-line, stackless traversal); -1 unknown
-  DevBuf scene, jump, rng_rows, rng_cols, rng_slot, rc, work, counters, wave_trace, tile_cost, tile_order;
+  DevBuf scene, jump, rng_rows, rng_cols, rng_slot, rc, work, counters, wave_trace, tile_cost, tile_order, prim_lists, prim_counts;
   // seeding tables of the last geometry, kept on the device: the phase bases (xorwow_phase_bases; key = seed, W,
   // rows of the shard) and the column tables (xorwow_column_tables; key = W)
   uint64_t rows_key[5] = {~0ull, 0, 0, 0, 0};
@@ -266,6 +273,19 @@ int rt_accel_build_wide(const rt_scene *scene, uint32_t *words, uint64_t cap, ui
   return RT_OK;
 }
 
+// max over the SAH prims of |motion| / 2 (rounded up a little)
+static double half_motion_of(const std::vector<uint32_t> &prims) {
+  double m = 0.0;
+  for (size_t k = 0; k + rt::kAccelPrimWords <= prims.size(); k += rt::kAccelPrimWords) {
+    float v[3];
+    std::memcpy(v, &prims[k + rt::AP_MOTION], sizeof v);
+    m = std::max(m, std::sqrt(static_cast<double>(v[0]) * v[0] + static_cast<double>(v[1]) * v[1] + static_cast<double>(v[2]) * v[2]));
+  }
+  return 0.5 * m * (1.0 + 1.0e-9);
+}
+
+static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p, uint32_t tiles_x, double half_motion, float *rho_f);
+
 int rt_accel_build_quant(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]) {
   if (!scene || !info) return RT_ERR_INVALID_ARG;
   rt::SceneImage img;
@@ -281,6 +301,31 @@ int rt_accel_build_quant(const rt_scene *scene, uint32_t *words, uint64_t cap, u
   if (words) {
     if (cap < a.wide_q_words.size()) return RT_ERR_INVALID_ARG;
     std::memcpy(words, a.wide_q_words.data(), a.wide_q_words.size() * 4);
+  }
+  return RT_OK;
+}
+
+int rt_prim_lists(const rt_scene *scene, const rt_camera *cam, const rt_params *p, uint32_t cap, uint32_t *counts,
+                  uint32_t *lists, float *rho) {
+  if (!scene || !cam || !p || !counts || cap == 0 || p->width <= 0 || p->row_count <= 0 || p->row_stride <= 0)
+    return RT_ERR_INVALID_ARG;
+  rt::SceneImage img;
+  int st = rt::compile_scene(scene, &img);
+  if (st != RT_OK) return st;
+  rt::SphereAccel a;
+  std::string why;
+  if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
+  const double motion = half_motion_of(a.prim_words);
+  const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
+  const uint32_t n_tiles = tiles_x * ((static_cast<uint32_t>(p->row_count) + 7) / 8);
+  float rf = 0.0f;
+  const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, motion, &rf);
+  if (rho) *rho = rf;
+  std::vector<uint2> buf(cap);
+  for (uint32_t t = 0; t < n_tiles; ++t) {
+    counts[t] = rt::prim_list_build_host(g, a.node_words.data(), a.root, a.prim_words.data(), t, cap, buf.data());
+    if (lists && counts[t] != rt::kPrimListNone)
+      for (uint32_t k = 0; k < counts[t]; ++k) { lists[(static_cast<size_t>(t) * cap + k) * 2] = buf[k].x; lists[(static_cast<size_t>(t) * cap + k) * 2 + 1] = buf[k].y; }
   }
   return RT_OK;
 }
@@ -326,7 +371,7 @@ void rt_context_destroy(rt_context *c) {
   {
     DeviceGuard g(c->device);
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
-    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->rng_slot.release(); c->rc.release();
+    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->prim_lists.release(); c->prim_counts.release(); c->rng_slot.release(); c->rc.release();
     c->work.release(); c->counters.release();
     c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
   }
@@ -354,6 +399,8 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->rc_lds_auto = false;
   }
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
+  if (const char *e = std::getenv("RT_ACCEL_PRIM")) c->prim_on = e[0] != '0';
+  if (const char *e = std::getenv("RT_PRIM_CAP")) c->prim_cap = static_cast<uint32_t>(std::max(1, std::min(256, std::atoi(e))));
   if (const char *e = std::getenv("RT_JIT_LANE")) c->lane_jit = e[0] != '0';
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
   if (const char *e = std::getenv("RT_MAX_TRIES")) c->max_tries = static_cast<uint32_t>(std::max(0, std::atoi(e)));
@@ -396,6 +443,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     dev_words.insert(dev_words.end(), c->accel.node_words.begin(), c->accel.node_words.end());
     c->accel_prims = static_cast<uint32_t>(dev_words.size());
     dev_words.insert(dev_words.end(), c->accel.prim_words.begin(), c->accel.prim_words.end());
+    c->accel_half_motion = half_motion_of(c->accel.prim_words);
     c->accel_w4 = rt::accel_width() == 4 && !c->accel.wide_words.empty();
     c->accel_q = c->accel_w4 && rt::accel_quant() && !c->accel.wide_q_words.empty();
     if (c->accel_w4) {
@@ -443,6 +491,31 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
 
 int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, float *out_dev, void *stream) {
   return rt_context_render_ppm(c, cam, p, out_dev, nullptr, stream);
+}
+
+// The ray cone geometry of a frame's camera for the primary-ray candidate lists (device/prim_lists.h): the defocus
+// disc's radius bound and the footprint widening cover the float arithmetic of the kernel's camera ray (a few
+// roundings of these magnitudes, far inside 2^-18 of them); *rho_f = the radius bound as a float, rounded up.
+static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p, uint32_t tiles_x, double half_motion, float *rho_f) {
+  rt::PrimListGeom g{};
+  const rtr_vec3 *cv[4] = {&cam->pixel00, &cam->delta_u, &cam->delta_v, &cam->center};
+  double *gd[4] = {g.p00, g.du, g.dv, g.c};
+  for (int k = 0; k < 4; ++k) { gd[k][0] = cv[k]->x; gd[k][1] = cv[k]->y; gd[k][2] = cv[k]->z; }
+  auto n1 = [](const rtr_vec3 &v) { return std::fabs(static_cast<double>(v.x)) + std::fabs(static_cast<double>(v.y)) + std::fabs(static_cast<double>(v.z)); };
+  auto sq = [](const rtr_vec3 &v) { return static_cast<double>(v.x) * v.x + static_cast<double>(v.y) * v.y + static_cast<double>(v.z) * v.z; };
+  const double l1 = n1(cam->center);
+  // origin = centre + x u + y v with x^2 + y^2 < 1 (:1459-1476): |origin - centre| <= sqrt(|u|^2 + |v|^2)
+  const double rho = cam->defocus_angle > 0 ? std::sqrt(sq(cam->defocus_u) + sq(cam->defocus_v)) : 0.0;
+  g.rho = rho * (1.0 + 0x1p-18) + 0x1p-18 * l1;
+  const double rows_span = static_cast<double>(p->row_offset) + static_cast<double>(p->row_count) * p->row_stride + 1.0;
+  g.eps = 0x1p-18 * (n1(cam->pixel00) + rows_span * n1(cam->delta_v) + (p->width + 1.0) * n1(cam->delta_u) + l1 + g.rho);
+  g.width = p->width; g.rows = p->row_count; g.row_offset = p->row_offset; g.row_stride = p->row_stride;
+  g.tiles_x = tiles_x;
+  g.half_motion = half_motion;
+  float fr = static_cast<float>(g.rho);
+  if (static_cast<double>(fr) < g.rho) fr = std::nextafter(fr, std::numeric_limits<float>::infinity());
+  *rho_f = fr;
+  return g;
 }
 
 int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *p, float *out_dev, uint8_t *out8_dev,
@@ -805,6 +878,36 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
 
   if (hipMemsetAsync(c->work.p, 0, 256, s) != hipSuccess) return RT_ERR_HIP;
   if (c->counted && hipMemsetAsync(c->counters.p, 0, RT_CNT__COUNT * 8, s) != hipSuccess) return RT_ERR_HIP;
+  a.prim_lists = nullptr;
+  a.prim_counts = nullptr;
+  if (trav == RT_TRAV_ACCEL && c->prim_on && c->accel_ok) {
+    // primary-ray candidate lists of this frame's camera (device/prim_lists.h), before the probe and the render
+    float prim_rho = 0.0f;
+    const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, c->accel_half_motion, &prim_rho);
+    if (c->prim_lists.ensure(static_cast<size_t>(n_tiles) * c->prim_cap * 8) != hipSuccess ||
+        c->prim_counts.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
+      return RT_ERR_HIP;
+    const uint32_t *sw = static_cast<const uint32_t *>(c->scene.p);
+    if (rt::launch_prim_lists(g, sw + c->accel_nodes, c->accel.root, sw + c->accel_prims, n_tiles, c->prim_cap,
+                              static_cast<uint2 *>(c->prim_lists.p), static_cast<uint32_t *>(c->prim_counts.p), s) != hipSuccess)
+      return RT_ERR_HIP;
+    a.prim_lists = static_cast<const uint32_t *>(c->prim_lists.p);
+    a.prim_counts = static_cast<const uint32_t *>(c->prim_counts.p);
+    a.prim_cap = c->prim_cap;
+    a.prim_rho = prim_rho;
+    if (std::getenv("RT_DEBUG")) {   // diagnostics only: a synchronous copy of the counts
+      std::vector<uint32_t> cnt(n_tiles);
+      if (hipStreamSynchronize(s) == hipSuccess &&
+          hipMemcpy(cnt.data(), c->prim_counts.p, cnt.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+        uint64_t with = 0, sum = 0, mx = 0;
+        for (uint32_t v : cnt)
+          if (v != rt::kPrimListNone) { ++with; sum += v; mx = std::max<uint64_t>(mx, v); }
+        std::fprintf(stderr, "[rt] primary lists: %llu of %u tiles, mean %.1f, max %llu spheres\n",
+                     static_cast<unsigned long long>(with), n_tiles, with ? static_cast<double>(sum) / with : 0.0,
+                     static_cast<unsigned long long>(mx));
+      }
+    }
+  }
   // no seeding launch: the render kernel seeds each pixel's state at tile pickup (init_ms is the empty interval)
   if (hipEventRecord(c->ev[0], s) != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[1], s) != hipSuccess) return RT_ERR_HIP;

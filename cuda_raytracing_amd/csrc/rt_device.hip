@@ -181,7 +181,82 @@ __global__ __launch_bounds__(256) void unpermute_kernel(const uint8_t *__restric
   }
 }
 
+// Primary-ray candidate lists of the verified sphere walk (device/prim_lists.h): one wave per 8x8 tile walks the SAH
+// tree breadth-first (a level's surviving nodes in LDS, one per lane), collects the spheres that meet the tile's ray
+// cone in LDS and writes them sorted (each entry's rank = the entries before it): the depth of the tree in
+// dependent node loads per tile, not a serial walk of every node the cone meets.
+constexpr uint32_t kPrimFrontier = 512;   // nodes of one BFS level per tile (more: no list, the rays walk)
+constexpr uint32_t kPrimMaxCap = 256;     // list capacity the kernel's LDS holds
+__global__ __launch_bounds__(64) void prim_list_kernel(PrimListGeom g, const uint32_t *nodes, uint32_t root,
+                                                       const uint32_t *prims, uint32_t n_tiles, uint32_t cap,
+                                                       uint2 *lists, uint32_t *counts) {
+  __shared__ uint32_t front[2][kPrimFrontier];
+  __shared__ uint2 cand[kPrimMaxCap];
+  __shared__ uint32_t n_next, n_cand, bad;
+  const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+  if (tile >= n_tiles) return;
+  PrimCone k;
+  if (!prim_cone(g, tile, &k)) {
+    if (lane == 0) counts[tile] = kPrimListNone;
+    return;
+  }
+  if (lane == 0) { front[0][0] = root; n_cand = 0; bad = 0; }
+  uint32_t n_cur = 1, cur = 0;
+  __syncthreads();
+  while (n_cur > 0) {
+    if (lane == 0) n_next = 0;
+    __syncthreads();
+    for (uint32_t i = lane; i < n_cur; i += 64) {
+      const uint32_t *nd = nodes + static_cast<size_t>(front[cur][i]) * kAccelNodeWords;
+      for (int ch = 0; ch < 2; ++ch) {
+        if (!prim_cone_child(k, g, nd, ch)) continue;
+        const uint32_t ref = nd[12 + ch];
+        if (!(ref & kAccelLeaf)) {
+          const uint32_t at = atomicAdd(&n_next, 1u);
+          if (at < kPrimFrontier) front[cur ^ 1][at] = ref;
+          else bad = 1;
+          continue;
+        }
+        const uint32_t first = ref & 0xffffffu, cnt = ((ref >> 24) & 0x7fu) + 1u;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          uint32_t key;
+          if (!prim_cone_sphere(k, g, prims, first + j, &key)) continue;
+          const uint32_t at = atomicAdd(&n_cand, 1u);
+          if (at < cap) cand[at] = make_uint2(first + j, key);
+          else bad = 1;
+        }
+      }
+    }
+    __syncthreads();
+    n_cur = n_next < kPrimFrontier ? n_next : kPrimFrontier;
+    cur ^= 1;
+    if (bad) break;
+  }
+  __syncthreads();
+  if (bad) {
+    if (lane == 0) counts[tile] = kPrimListNone;
+    return;
+  }
+  const uint32_t n = n_cand;
+  uint2 *out = lists + static_cast<size_t>(tile) * cap;
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint2 e = cand[i];
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < n; ++j) rank += prim_before(cand[j], e) ? 1u : 0u;
+    out[rank] = e;
+  }
+  if (lane == 0) counts[tile] = n;
+}
+
 }  // namespace
+
+hipError_t launch_prim_lists(const PrimListGeom &g, const uint32_t *nodes, uint32_t root, const uint32_t *prims,
+                             uint32_t n_tiles, uint32_t cap, uint2 *lists, uint32_t *counts, hipStream_t s) {
+  if (n_tiles == 0) return hipSuccess;
+  if (cap == 0 || cap > kPrimMaxCap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(prim_list_kernel, dim3(n_tiles), dim3(64), 0, s, g, nodes, root, prims, n_tiles, cap, lists, counts);
+  return hipGetLastError();
+}
 
 hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t n, uint32_t max_rows,
                             uint32_t row_bytes, hipStream_t s) {

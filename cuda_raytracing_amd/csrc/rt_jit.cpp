@@ -319,8 +319,15 @@ std::string jit_lane_source(const SceneImage &img, int variant) {
   return src;
 }
 
+// RT_JIT_MAX_VGPR=N caps every run-time render kernel at 2N VGPRs (amdgpu_num_vgpr, A/B)
+// waves > 0: amdgpu_waves_per_eu(waves); waves < 0: a cap of -waves VGPRs (amdgpu_num_vgpr counts register pairs of
+// the unified VGPR/AGPR file on gfx950: N gives 2N VGPRs)
 std::string waves_attr_n(int waves) {
-  return waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : waves_attr();
+  if (waves < 0) return " __attribute__((amdgpu_num_vgpr(" + std::to_string(-waves / 2) + ")))";
+  std::string a = waves > 0 ? " __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))" : waves_attr();
+  if (const char *e = std::getenv("RT_JIT_MAX_VGPR"))
+    if (std::atoi(e) > 0) a += " __attribute__((amdgpu_num_vgpr(" + std::to_string(std::atoi(e)) + ")))";
+  return a;
 }
 
 std::string jit_accel_source(const SceneImage &img, int variant, int waves, int wide) {
@@ -356,13 +363,14 @@ std::string jit_mixed_source(const SceneImage &img, int variant, int waves) {
 }
 
 // One residency step for a few registers: the allocator often lands just above a boundary of the hardware's
-// 16-VGPR granule (the 10k walk at 82 VGPRs = 5 waves/SIMD, 80 would be 6; the mixed walk at 98 = 4, 96 would
-// be 5).  When the render kernel is within kRaiseSlack VGPRs of the next residency, its module is rebuilt
-// with amdgpu_waves_per_eu(that residency) and kept if the kernel then reaches it with at most kRaiseScratch bytes
-// of scratch per lane (a couple of spilled values outside the hot loops; round 4: the static kernels of scene 0 and
-// the Cornell box land at 81-85 VGPRs, one step above 6 waves).  RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves
-// the first build.
-constexpr int kRaiseSlack = 8;
+// 16-VGPR granule (the 10k walk at 82 VGPRs = 5 waves/SIMD, 80 would be 6; the mixed walk at 169 = 2, 160 would
+// be 3).  When the render kernel is within kRaiseSlack VGPRs of the next residency, its module is rebuilt with
+// that residency's register cap (amdgpu_num_vgpr: the waves-per-EU request budgets with an 8-VGPR granule, 168
+// for 3 waves, which the hardware's granule does not fit) and kept if the kernel then reaches it with at most
+// kRaiseScratch bytes of scratch per lane (a few spilled values outside the hot loops; round 4: the static
+// kernels of scene 0 and the Cornell box land at 81-85 VGPRs, the mixed walk of final_scene at 169).
+// RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves the first build.
+constexpr int kRaiseSlack = 12;
 constexpr int kRaiseScratch = 16;
 
 int render_vgprs(hipFunction_t fn, int *scratch) {
@@ -373,31 +381,29 @@ int render_vgprs(hipFunction_t fn, int *scratch) {
   return v;
 }
 
+// source(n): the module's source with the render kernel's attribute waves_attr_n(n) (n < 0: a cap of -n VGPRs)
 template <class Source>
 void raise_residency(const Source &source, const char *prefix, JitKernels *out) {
-  if (std::getenv("RT_JIT_WAVES")) return;
+  if (std::getenv("RT_JIT_WAVES") || std::getenv("RT_JIT_MAX_VGPR")) return;
   if (const char *e = std::getenv("RT_JIT_RAISE")) if (e[0] == '0') return;
   int sc0 = 0;
   const int v0 = render_vgprs(out->render, &sc0);
   if (v0 <= 0 || sc0 < 0 || sc0 > kRaiseScratch) return;
   const int cur = resident_blocks_by_vgprs(v0);
-  for (int w = cur + 1; w <= 8; ++w) {
-    const int limit = 512 / w / 8 * 8;   // the allocator's budget for w waves (granule 8)
-    if (resident_blocks_by_vgprs(limit) <= cur) continue;
-    if (v0 - limit > kRaiseSlack) return;
-    JitKernels k = *out;
-    std::string why;
-    if (!build_module(source(w), prefix, &k, &why)) return;
-    int sc = 0;
-    const int v = render_vgprs(k.render, &sc);
-    if (std::getenv("RT_DEBUG"))
-      std::fprintf(stderr, "[rt] jit residency raise %s: %d VGPRs (%d/CU) -> waves_per_eu(%d): %d VGPRs, scratch %d B\n",
-                   prefix, v0, cur, w, v, sc);
-    if (v > 0 && sc >= 0 && sc <= kRaiseScratch && resident_blocks_by_vgprs(v) > cur) {
-      k.ms += out->ms;
-      *out = k;
-    }
-    return;
+  if (cur >= 8) return;
+  const int limit = 512 / (cur + 1) / 16 * 16;   // the hardware's budget for one more wave per SIMD
+  if (v0 - limit > kRaiseSlack) return;
+  JitKernels k = *out;
+  std::string why;
+  if (!build_module(source(-limit), prefix, &k, &why)) return;
+  int sc = 0;
+  const int v = render_vgprs(k.render, &sc);
+  if (std::getenv("RT_DEBUG"))
+    std::fprintf(stderr, "[rt] jit residency raise %s: %d VGPRs (%d/SIMD) -> cap %d: %d VGPRs, scratch %d B\n",
+                 prefix, v0, cur, limit, v, sc);
+  if (v > 0 && sc >= 0 && sc <= kRaiseScratch && resident_blocks_by_vgprs(v) > cur) {
+    k.ms += out->ms;
+    *out = k;
   }
 }
 
@@ -447,10 +453,11 @@ int accel_width() {
   return 2;
 }
 
-// The 4-wide tree quantised (accel::quantize_wide, 64-B nodes) or as float planes (128-B nodes): RT_ACCEL_QUANT=0/1
+// The 4-wide tree quantised (accel::quantize_wide, 64-B nodes; RT_ACCEL_QUANT=1) or as float planes (128-B nodes,
+// default): measured on the 10k config, the quantised walk is 15 % slower than the float one
 bool accel_quant() {
   if (const char *e = std::getenv("RT_ACCEL_QUANT")) return e[0] != '0';
-  return true;
+  return false;
 }
 
 // The default 6-wave request is measured on the plain 10k walk, whose 80-VGPR build spills ~17 VGPRs outside

@@ -40,7 +40,7 @@ std::string jit_lane_source(const SceneImage &img, int variant);
 bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why);   // wide: 0 BVH2, 1 4-wide, 2 quantised 4-wide
 std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0, int wide = 0);   // waves > 0: amdgpu_waves_per_eu
 int accel_width();   // 2 or 4 (RT_ACCEL_WIDTH)
-bool accel_quant();  // the 4-wide tree quantised (RT_ACCEL_QUANT, default on)
+bool accel_quant();  // the 4-wide tree quantised (RT_ACCEL_QUANT, default off)
 int accel_waves();   // the verified sphere walk's waves per SIMD request (6; RT_ACCEL_WAVES, 0 = allocator's choice)
 // verified mixed-world traversal kernels (MixedTraceK over the scene's node kinds)
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);

@@ -235,10 +235,18 @@ int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_
  * needed): info = {wide nodes, depth, stack bound of the ordered walk, node words}; words (if non-null, cap
  * words) receives the node words.  RT_ERR_UNSUPPORTED when the world is not eligible. */
 int rt_accel_build_wide(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
-/* The 4-wide tree quantised (the verified walk's default 4-wide form, RT_ACCEL_QUANT; device/rt_layout.h kAccel4Q*,
+/* The 4-wide tree quantised (the verified walk's RT_ACCEL_QUANT=1 form; device/rt_layout.h kAccel4Q*,
  * one 64-B line per node; no device needed): info and words as rt_accel_build_wide's, same node numbering.
  * RT_ERR_UNSUPPORTED when the world is not eligible or its boxes exceed the quantiser's exponent range. */
 int rt_accel_build_quant(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]);
+/* The verified sphere walk's primary-ray candidate lists of a frame, built on the host with the code the device
+ * runs per frame (device/prim_lists.h; no device needed; tests): for every 8x8 tile of the shard p describes,
+ * counts[tile] = entries (0xffffffff: no list, the tile's camera rays walk the tree) and, if lists is non-null,
+ * lists[(tile * cap + k) * 2 + {0, 1}] = {sphere index in the SAH prim order, axial lower bound as float bits},
+ * ascending; *rho (if non-null) = the origin radius bound the kernel's early exit uses.  RT_ERR_UNSUPPORTED when
+ * the world is not eligible for the verified sphere walk. */
+int rt_prim_lists(const rt_scene *scene, const rt_camera *cam, const rt_params *p, uint32_t cap, uint32_t *counts,
+                  uint32_t *lists, float *rho);
 /* The per-pixel XORWOW states rt_render seeds on the device (init_gpu_data's curand_init,
  * raytracing.cu:1591-1606, subsequence = global pixel index), for rows row_offset + k*row_stride,
  * k < rows, of a width-wide frame: out_states (host) receives [6][rows*width] words {d, x0..x4}.

@@ -197,3 +197,104 @@ def test_quantised_wide_tree_contains_the_float_boxes(idx):
                 lo, hi = org[a] + ql * step, org[a] + qh * step
                 assert lo <= box[2 * a] - ep and hi >= box[2 * a + 1] + ep, (a, c)
                 assert lo > box[2 * a] - ep - 2 * step and hi < box[2 * a + 1] + ep + 2 * step, (a, c)
+
+
+def _cam_vecs(cam):
+    v = lambda x: np.array(x.tolist(), np.float32)  # noqa: E731
+    return (v(cam.pixel00), v(cam.delta_u), v(cam.delta_v), v(cam.center), v(cam.defocus_u), v(cam.defocus_v))
+
+
+def _random_moving_world(seed):
+    g = np.random.default_rng(500 + seed)
+    w = rt.World(capacity=1024)
+    m = w.lambert((0.5, 0.5, 0.5))
+    w.sphere((0.0, -1000.0, 0.0), 1000.0, m)
+    for k in range(int(g.integers(80, 300))):
+        c = (float(g.uniform(-6, 6)), float(g.uniform(0, 3)), float(g.uniform(-6, 6)))
+        r = float(g.choice([0.05, 0.3, 1.0]))
+        if k % 9 == 0:
+            w.moving_sphere(c, (0.0, float(g.uniform(0, 0.6)), 0.0), r, m)
+        else:
+            w.sphere(c, r, m)
+    s = rt.Settings()
+    import ctypes as C
+    from cuda_raytracing_amd import _abi
+    _abi.host_lib().rt_settings_default(C.byref(s))
+    s.lookfrom = rt.vec3(float(g.uniform(-10, 10)), float(g.uniform(1, 5)), float(g.uniform(-10, 10)))
+    s.lookat = rt.vec3(0.0, 0.5, 0.0)
+    s.vfov = float(g.uniform(25, 60))
+    s.defocus_angle = float(g.choice([0.0, 0.6, 3.0]))
+    return w, s
+
+
+@pytest.mark.parametrize("case", ["10k", "10k_shard", "rand0", "rand1", "rand2"])
+def test_primary_candidate_lists_hold_every_hit(case):
+    # device/prim_lists.h (built here on the host by the same code): for camera rays of each tile, generated in
+    # float32 as the kernel does (defocus disc, pixel jitter), the closest sphere by brute force over every sphere
+    # is in the tile's list, and its axial bound lies within rho + t |d| (the kernel's early exit keeps it)
+    if case.startswith("10k"):
+        w, s = rt.build_scene(rt.RT_SCENE_RANDOM_10K)
+        W, H = 320, 180
+    else:
+        w, s = _random_moving_world(int(case[-1]))
+        W, H = 96, 64
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    off, stride, rows = (1, 3, (H - 1) // 3) if case == "10k_shard" else (0, 1, H)
+    p = rt.make_params(s, W, H, spp=1, bounces=4, row_offset=off, row_stride=stride, row_count=rows)
+    res = rt.prim_lists(w.scene(), cam, p, cap=256)
+    assert res is not None
+    counts, lists, rho = res
+    _, _, prims = rt.accel_build(w.scene())
+    P = prims.reshape(-1, 16)
+    pc = f(P[:, 0:3]).astype(np.float64)
+    mv = f(P[:, 3:6]).astype(np.float64)
+    rad2 = f(P[:, 6]).astype(np.float64)
+    p00, du, dv, C0, dfu, dfv = _cam_vecs(cam)
+    g = np.random.default_rng(7)
+    tiles_x = (W + 7) // 8
+    assert (counts != 0xFFFFFFFF).mean() > 0.9
+    checked = 0
+    for t in range(len(counts)):
+        if counts[t] == 0xFFFFFFFF:
+            continue
+        n = int(counts[t])
+        ids = lists[t, :n, 0].astype(np.int64)
+        bnd = f(lists[t, :n, 1]).astype(np.float64)
+        assert np.all(np.diff(bnd) >= 0)
+        ty, tx = divmod(t, tiles_x)
+        for _ in range(3):
+            lr = min(ty * 8 + int(g.integers(0, 8)), rows - 1)
+            j = min(tx * 8 + int(g.integers(0, 8)), W - 1)
+            i = off + lr * stride
+            if cam.defocus_angle > 0:
+                while True:
+                    y, x = np.float32(g.uniform(-1, 1)), np.float32(g.uniform(-1, 1))
+                    if x * x + y * y < 1:
+                        break
+                O = C0 + (x * dfu + y * dfv)
+            else:
+                O = C0
+            xo, yo = np.float32(g.uniform(-0.5, 0.5)), np.float32(g.uniform(-0.5, 0.5))
+            pp = p00 + (np.float32(i) * dv + np.float32(j) * du)
+            D = ((pp - O) + xo * du) + yo * dv
+            tm = np.float64(g.uniform(0, 1))
+            o, d = O.astype(np.float64), D.astype(np.float64)
+            c = pc + tm * mv
+            oc = c - o
+            a = d @ d
+            b = -2 * (oc @ d)
+            cc = (oc * oc).sum(1) - rad2
+            disc = b * b - 4 * a * cc
+            ok = disc >= 0
+            sq = np.sqrt(np.where(ok, disc, 0))
+            r1, r2 = (-b - sq) / (2 * a), (-b + sq) / (2 * a)
+            root = np.where(r1 > 1e-3, r1, r2)
+            root = np.where(ok & (root > 1e-3), root, np.inf)
+            k = int(root.argmin())
+            if not np.isfinite(root[k]):
+                continue
+            assert k in set(ids.tolist()), (t, k)
+            pos = int(np.nonzero(ids == k)[0][0])
+            assert bnd[pos] <= rho + root[k] * np.sqrt(a), (t, k)
+            checked += 1
+    assert checked > 100

@@ -1004,7 +1004,7 @@ def test_kernel_span_within_event_window():
 
 
 # ---- the verified sphere walk over the 4-wide tree (RT_ACCEL_WIDTH=4, accel::collapse_wide) ----
-# (quantised 64-B nodes by default, accel::quantize_wide; RT_ACCEL_QUANT=0: the float 128-B nodes)
+# (float 128-B nodes by default; RT_ACCEL_QUANT=1: the quantised 64-B nodes, accel::quantize_wide)
 @pytest.mark.parametrize("idx,W,H,spp,quant", [(2, 64, 36, 4, "1"), (20, 160, 90, 6, "1"), (20, 480, 270, 4, "1"),
                                                (2, 64, 36, 4, "0"), (20, 160, 90, 6, "0")])
 def test_wide_verified_sphere_traversal_matches_oracle(idx, W, H, spp, quant, monkeypatch):
@@ -1058,3 +1058,40 @@ def test_byte_colour_codes_all_levels_in_lds(byte, monkeypatch):
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
     if byte == "1":
         assert st.rc_lds_levels >= 50 and st.rc_hbm_slots == 0, (st.rc_lds_levels, st.rc_hbm_slots)
+
+
+# ---- primary-ray candidate lists of the verified sphere walk (device/prim_lists.h, RT_ACCEL_PRIM) ----
+@pytest.mark.parametrize("idx,W,H,spp", [(20, 160, 90, 4), (2, 96, 54, 4)])
+def test_primary_candidate_lists_match_oracle(idx, W, H, spp, monkeypatch):
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0
+    fb, st = gpu(w.scene(), cam, p)
+    assert st.traversal == rt.RT_TRAV_ACCEL and np.array_equal(bits(fb), bits(ref))
+    # a row shard (lists per shard tile: taller footprints)
+    ps = rt.make_params(s, W, H, spp=spp, bounces=16, row_offset=1, row_stride=3, flags=rt.RT_FLAG_FORCE_ACCEL)
+    rc, refs, _ = oracle_render(w.scene(), cam, ps)
+    fs, _ = gpu(w.scene(), cam, ps)
+    assert np.array_equal(bits(fs), bits(refs))
+    # the camera rays take the lists: fewer executed node visits than with the lists off, same reference counts
+    pc = rt.make_params(s, W, H, spp=2, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL | rt.RT_FLAG_COUNT)
+    _, on = gpu(w.scene(), cam, pc)
+    monkeypatch.setenv("RT_ACCEL_PRIM", "0")
+    fo, _ = gpu(w.scene(), cam, p)
+    _, off = gpu(w.scene(), cam, pc)
+    a, b = on.counter_dict(), off.counter_dict()
+    assert np.array_equal(bits(fo), bits(ref))
+    assert a["visit_bvh"] == b["visit_bvh"] and a["exec_node"] < b["exec_node"], (a, b)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_primary_candidate_lists_random_worlds(seed):
+    # moving spheres, duplicates, defocus (the random verified-walk worlds): bit-exact with the lists on
+    w, s = _random_sphere_world(seed)
+    cam, W, H = rt.camera_from_settings(s, 64, 36)
+    p = rt.make_params(s, W, H, spp=4, bounces=12, flags=rt.RT_FLAG_FORCE_ACCEL)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    fb, st = gpu(w.scene(), cam, p)
+    assert rc == 0 and st.traversal == rt.RT_TRAV_ACCEL and np.array_equal(bits(fb), bits(ref))
