@@ -971,16 +971,20 @@ struct AccelTraceK {
         if (n <= A.prim_cap) {
           walking = false;
           const float dl = sqrtf(dot(r.d, r.d));
-          const uint2 *L = reinterpret_cast<const uint2 *>(A.prim_lists) + static_cast<size_t>(tile) * A.prim_cap;
+          const uint32_t q = A.prim_words >> 2;   // uint4 per entry
+          const uint4 *L = reinterpret_cast<const uint4 *>(A.prim_lists) + static_cast<size_t>(tile) * A.prim_cap * q;
+          // entry k's words loaded one iteration ahead (its loads under entry k-1's test)
+          uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
+          if (n > 0) { e0 = L[0]; e1 = L[1]; }
           for (uint32_t k = 0; k < n; ++k) {
-            const uint2 e = L[k];
-            if (__uint_as_float(e.y) > __builtin_fmaf(T.tmax, dl, A.prim_rho) * 1.0000010f) break;
+            const uint4 a0 = e0, a1 = e1;
+            const uint32_t e2z = q > 2 ? L[k * q + 2].x : 0u;
+            if (k + 1 < n) { e0 = L[(k + 1) * q]; e1 = L[(k + 1) * q + 1]; }
+            if (__uint_as_float(a1.y) > __builtin_fmaf(T.tmax, dl, A.prim_rho) * 1.0000010f) break;
             if (COUNT) vc.xp++;
-            const uint32_t pr = e.x;
-            const uint4 p0 = P[pr * 4], pw1 = P[pr * 4 + 1], pw2 = P[pr * 4 + 2];
-            if (sphere_hit_tie<UV, true, false>(T, r, h, pw2.x, mk(asf(p0.x), asf(p0.y), asf(p0.z)),
-                                                mk(asf(p0.w), asf(pw1.x), asf(pw1.y)), asf(pw1.z), asf(pw1.w), sa2, sra2, tie))
-              best = pr;
+            if (sphere_hit_tie<UV, true, false>(T, r, h, 0u, mk(asf(a0.x), asf(a0.y), asf(a0.z)),
+                                                mk(asf(a1.z), asf(a1.w), asf(e2z)), asf(a0.w), 0.0f, sa2, sra2, tie))
+              best = a1.x;
           }
         }
       }

@@ -884,13 +884,15 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     // primary-ray candidate lists of this frame's camera (device/prim_lists.h), before the probe and the render
     float prim_rho = 0.0f;
     const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, c->accel_half_motion, &prim_rho);
-    if (c->prim_lists.ensure(static_cast<size_t>(n_tiles) * c->prim_cap * 8) != hipSuccess ||
+    const uint32_t words = c->accel_half_motion > 0 ? 12u : 8u;
+    if (c->prim_lists.ensure(static_cast<size_t>(n_tiles) * c->prim_cap * words * 4) != hipSuccess ||
         c->prim_counts.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
       return RT_ERR_HIP;
     const uint32_t *sw = static_cast<const uint32_t *>(c->scene.p);
-    if (rt::launch_prim_lists(g, sw + c->accel_nodes, c->accel.root, sw + c->accel_prims, n_tiles, c->prim_cap,
-                              static_cast<uint2 *>(c->prim_lists.p), static_cast<uint32_t *>(c->prim_counts.p), s) != hipSuccess)
+    if (rt::launch_prim_lists(g, sw + c->accel_nodes, c->accel.root, sw + c->accel_prims, n_tiles, c->prim_cap, words,
+                              static_cast<uint32_t *>(c->prim_lists.p), static_cast<uint32_t *>(c->prim_counts.p), s) != hipSuccess)
       return RT_ERR_HIP;
+    a.prim_words = words;
     a.prim_lists = static_cast<const uint32_t *>(c->prim_lists.p);
     a.prim_counts = static_cast<const uint32_t *>(c->prim_counts.p);
     a.prim_cap = c->prim_cap;

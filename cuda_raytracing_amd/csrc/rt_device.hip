@@ -189,7 +189,7 @@ constexpr uint32_t kPrimFrontier = 512;   // nodes of one BFS level per tile (mo
 constexpr uint32_t kPrimMaxCap = 256;     // list capacity the kernel's LDS holds
 __global__ __launch_bounds__(64) void prim_list_kernel(PrimListGeom g, const uint32_t *nodes, uint32_t root,
                                                        const uint32_t *prims, uint32_t n_tiles, uint32_t cap,
-                                                       uint2 *lists, uint32_t *counts) {
+                                                       uint32_t words, uint32_t *lists, uint32_t *counts) {
   __shared__ uint32_t front[2][kPrimFrontier];
   __shared__ uint2 cand[kPrimMaxCap];
   __shared__ uint32_t n_next, n_cand, bad;
@@ -238,12 +238,18 @@ __global__ __launch_bounds__(64) void prim_list_kernel(PrimListGeom g, const uin
     return;
   }
   const uint32_t n = n_cand;
-  uint2 *out = lists + static_cast<size_t>(tile) * cap;
+  uint32_t *out = lists + static_cast<size_t>(tile) * cap * words;
   for (uint32_t i = lane; i < n; i += 64) {
     const uint2 e = cand[i];
     uint32_t rank = 0;
     for (uint32_t j = 0; j < n; ++j) rank += prim_before(cand[j], e) ? 1u : 0u;
-    out[rank] = e;
+    // the entry with the sphere inline (rt_layout.h kPrimEntry*)
+    const uint32_t *pw = prims + static_cast<size_t>(e.x) * kAccelPrimWords;
+    uint32_t *o = out + static_cast<size_t>(rank) * words;
+    o[0] = pw[AP_CENTER]; o[1] = pw[AP_CENTER + 1]; o[2] = pw[AP_CENTER + 2]; o[3] = pw[AP_RADIUS2];
+    o[kPrimEntryIdx] = e.x; o[kPrimEntryBound] = e.y;
+    o[kPrimEntryMotion] = pw[AP_MOTION]; o[kPrimEntryMotion + 1] = pw[AP_MOTION + 1];
+    if (words > 8) { o[8] = pw[AP_MOTION + 2]; o[9] = 0; o[10] = 0; o[11] = 0; }
   }
   if (lane == 0) counts[tile] = n;
 }
@@ -251,10 +257,12 @@ __global__ __launch_bounds__(64) void prim_list_kernel(PrimListGeom g, const uin
 }  // namespace
 
 hipError_t launch_prim_lists(const PrimListGeom &g, const uint32_t *nodes, uint32_t root, const uint32_t *prims,
-                             uint32_t n_tiles, uint32_t cap, uint2 *lists, uint32_t *counts, hipStream_t s) {
+                             uint32_t n_tiles, uint32_t cap, uint32_t words, uint32_t *lists, uint32_t *counts,
+                             hipStream_t s) {
   if (n_tiles == 0) return hipSuccess;
-  if (cap == 0 || cap > kPrimMaxCap) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(prim_list_kernel, dim3(n_tiles), dim3(64), 0, s, g, nodes, root, prims, n_tiles, cap, lists, counts);
+  if (cap == 0 || cap > kPrimMaxCap || (words != 8 && words != 12)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(prim_list_kernel, dim3(n_tiles), dim3(64), 0, s, g, nodes, root, prims, n_tiles, cap, words, lists,
+                     counts);
   return hipGetLastError();
 }
 

@@ -18,8 +18,10 @@ hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s);
 hipError_t launch_render(const RenderArgs &a, int variant, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 // primary-ray candidate lists of the verified sphere walk, one per 8x8 tile of the shard (device/prim_lists.h)
+// (entries of `words` words with the sphere inline, rt_layout.h kPrimEntry*)
 hipError_t launch_prim_lists(const PrimListGeom &g, const uint32_t *nodes, uint32_t root, const uint32_t *prims,
-                             uint32_t n_tiles, uint32_t cap, uint2 *lists, uint32_t *counts, hipStream_t s);
+                             uint32_t n_tiles, uint32_t cap, uint32_t words, uint32_t *lists, uint32_t *counts,
+                             hipStream_t s);
 // multi-device frames: frame row k <- row k / n of shard k % n in src ([n][max_rows][row_bytes])
 hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t n, uint32_t max_rows,
                             uint32_t row_bytes, hipStream_t s);
