@@ -71,6 +71,7 @@ static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::
 
 constexpr int kLptMinSpp = 16;
 constexpr uint32_t kAccelMinSpheres = 64;   // smaller all-sphere worlds: the scene-specialised walk
+constexpr uint32_t kPrimMinSpheres = 2048;  // primary-ray candidate lists by default from this many spheres
 constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
@@ -160,7 +161,9 @@ struct rt_context {
   uint32_t accel_lds_nodes = 64;
   bool accel_lds_set = false;   // RT_ACCEL_LDS_NODES given (nodes of the tree in use)
   // primary-ray candidate lists of the verified sphere walk (device/prim_lists.h; RT_ACCEL_PRIM=0: off)
-  bool prim_on = true;
+  // -1 auto: worlds of at least kPrimMinSpheres spheres (measured: 10k scene -2 % frame time, the 488-sphere scene 2
+  // +4 %); 0 off, 1 on (RT_ACCEL_PRIM)
+  int prim_mode = -1;
   uint32_t prim_cap = 128;      // entries per tile (RT_PRIM_CAP); a fuller tile's rays walk the tree
   double accel_half_motion = 0;   // max |motion| / 2 over the SAH tree's spheres
   // verified mixed-world traversal (RT_TRAV_MIXED): macro roots marked in the image, SAH words appended
@@ -399,7 +402,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->rc_lds_auto = false;
   }
   if (const char *e = std::getenv("RT_BLOCKS_PER_CU")) c->blocks_per_cu = std::atoi(e);
-  if (const char *e = std::getenv("RT_ACCEL_PRIM")) c->prim_on = e[0] != '0';
+  if (const char *e = std::getenv("RT_ACCEL_PRIM")) c->prim_mode = e[0] != '0' ? 1 : 0;
   if (const char *e = std::getenv("RT_PRIM_CAP")) c->prim_cap = static_cast<uint32_t>(std::max(1, std::min(256, std::atoi(e))));
   if (const char *e = std::getenv("RT_JIT_LANE")) c->lane_jit = e[0] != '0';
   if (const char *e = std::getenv("RT_JIT_SHADE")) c->shade_spec = e[0] != '0';
@@ -880,7 +883,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (c->counted && hipMemsetAsync(c->counters.p, 0, RT_CNT__COUNT * 8, s) != hipSuccess) return RT_ERR_HIP;
   a.prim_lists = nullptr;
   a.prim_counts = nullptr;
-  if (trav == RT_TRAV_ACCEL && c->prim_on && c->accel_ok) {
+  const bool prim_on = c->prim_mode == 1 || (c->prim_mode < 0 && c->accel_ok && c->accel.spheres >= kPrimMinSpheres);
+  if (trav == RT_TRAV_ACCEL && prim_on && c->accel_ok) {
     // primary-ray candidate lists of this frame's camera (device/prim_lists.h), before the probe and the render
     float prim_rho = 0.0f;
     const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, c->accel_half_motion, &prim_rho);

@@ -1063,6 +1063,7 @@ def test_byte_colour_codes_all_levels_in_lds(byte, monkeypatch):
 # ---- primary-ray candidate lists of the verified sphere walk (device/prim_lists.h, RT_ACCEL_PRIM) ----
 @pytest.mark.parametrize("idx,W,H,spp", [(20, 160, 90, 4), (2, 96, 54, 4)])
 def test_primary_candidate_lists_match_oracle(idx, W, H, spp, monkeypatch):
+    monkeypatch.setenv("RT_ACCEL_PRIM", "1")   # (default: worlds of >= 2048 spheres)
     w, s = rt.build_scene(idx)
     cam, W, H = rt.camera_from_settings(s, W, H)
     p = rt.make_params(s, W, H, spp=spp, bounces=16, flags=rt.RT_FLAG_FORCE_ACCEL)
@@ -1087,8 +1088,9 @@ def test_primary_candidate_lists_match_oracle(idx, W, H, spp, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2, 3])
-def test_primary_candidate_lists_random_worlds(seed):
+def test_primary_candidate_lists_random_worlds(seed, monkeypatch):
     # moving spheres, duplicates, defocus (the random verified-walk worlds): bit-exact with the lists on
+    monkeypatch.setenv("RT_ACCEL_PRIM", "1")
     w, s = _random_sphere_world(seed)
     cam, W, H = rt.camera_from_settings(s, 64, 36)
     p = rt.make_params(s, W, H, spp=4, bounces=12, flags=rt.RT_FLAG_FORCE_ACCEL)
