@@ -968,11 +968,13 @@ struct AccelTraceK {
       if (!resume && T.atie != 0u) {
         const uint32_t tile = T.atie - 1u;
         const uint32_t n = A.prim_counts[tile];
-        if (n <= A.prim_cap) {
+        const uint32_t cap = A.prim_cap;
+        if (n <= cap) {
           walking = false;
           const float dl = sqrtf(dot(r.d, r.d));
           const uint32_t q = A.prim_words >> 2;   // uint4 per entry
-          const uint4 *L = reinterpret_cast<const uint4 *>(A.prim_lists) + static_cast<size_t>(tile) * A.prim_cap * q;
+          const float rho = A.prim_rho;
+          const uint4 *L = reinterpret_cast<const uint4 *>(A.prim_lists) + static_cast<size_t>(tile) * cap * q;
           // entry k's words loaded one iteration ahead (its loads under entry k-1's test)
           uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
           if (n > 0) { e0 = L[0]; e1 = L[1]; }
@@ -980,7 +982,7 @@ struct AccelTraceK {
             const uint4 a0 = e0, a1 = e1;
             const uint32_t e2z = q > 2 ? L[k * q + 2].x : 0u;
             if (k + 1 < n) { e0 = L[(k + 1) * q]; e1 = L[(k + 1) * q + 1]; }
-            if (__uint_as_float(a1.y) > __builtin_fmaf(T.tmax, dl, A.prim_rho) * 1.0000010f) break;
+            if (__uint_as_float(a1.y) > __builtin_fmaf(T.tmax, dl, rho) * 1.0000010f) break;
             if (COUNT) vc.xp++;
             if (sphere_hit_tie<UV, true, false>(T, r, h, 0u, mk(asf(a0.x), asf(a0.y), asf(a0.z)),
                                                 mk(asf(a1.z), asf(a1.w), asf(e2z)), asf(a0.w), 0.0f, sa2, sra2, tie))
@@ -1790,7 +1792,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const bool probe = (F & kVarProbe) != 0 || ((F & kVarNoProbe) == 0 && A.probe_cost != nullptr);
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
-  const uint64_t t_wave0 = __builtin_amdgcn_s_memrealtime();   // kernel-only span (A.span)
+  // kernel-only span (A.span): the first wave's start is recorded at once (no 64-bit value held to the end)
+  if (A.span && __lane_id() == 0)
+    atomicMax(A.span, static_cast<unsigned long long>(~__builtin_amdgcn_s_memrealtime()));
   Mem<LDS> S{A.scene};
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
@@ -1870,7 +1874,6 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   uint32_t c_bounce = 0, c_shade = 0, c_perlin = 0, c_samples = 0;
 
   uint32_t chunk_pos = 0, chunk_end = 0;   // wave-uniform: ids of the wave's current tile
-  uint32_t chunk_base = 0;                 // wave-uniform: the first id of the chunk whose states are in the slot
   // the wave's slot: a wave-uniform base (scalar registers; threadIdx.x >> 6 is not known to be uniform) and
   // 32-bit per-lane offsets
   char *const rng_slot = reinterpret_cast<char *>(A.rng_slot) +
@@ -2009,13 +2012,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(A.rng_nib), 0,
                                                                               0x7fffffff, 0x00020000);
           rng_jump_nib(rs, tcol * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
-          *reinterpret_cast<uint32_t *>(rng_slot + lane * 4u) = x0;
-          *reinterpret_cast<uint32_t *>(rng_slot + 256u + lane * 4u) = x1;
-          *reinterpret_cast<uint32_t *>(rng_slot + 512u + lane * 4u) = x2;
-          *reinterpret_cast<uint32_t *>(rng_slot + 768u + lane * 4u) = x3;
-          *reinterpret_cast<uint32_t *>(rng_slot + 1024u + lane * 4u) = x4;
+          // slot entry id & 63: a chunk is size-aligned (whole tiles, or prio_chunk pieces, a power of two <= 64),
+          // so its ids take distinct entries and no chunk base is kept across rounds
+          const uint32_t so = (id & 63u) * 4u;
+          *reinterpret_cast<uint32_t *>(rng_slot + so) = x0;
+          *reinterpret_cast<uint32_t *>(rng_slot + 256u + so) = x1;
+          *reinterpret_cast<uint32_t *>(rng_slot + 512u + so) = x2;
+          *reinterpret_cast<uint32_t *>(rng_slot + 768u + so) = x3;
+          *reinterpret_cast<uint32_t *>(rng_slot + 1024u + so) = x4;
           __threadfence_block();   // the stores reach the wave's later loads of other lanes' entries
-          chunk_base = base;
         }
       }
       const uint32_t avail = chunk_end - chunk_pos;
@@ -2050,7 +2055,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
           } else {
             // the state seeded at the chunk's pickup (the slot entry of this id)
-            const uint32_t so = (id - chunk_base) * 4u;
+            const uint32_t so = (id & 63u) * 4u;
             rng.d = A.rng_d;
             rng.x0 = *reinterpret_cast<const uint32_t *>(rng_slot + so);
             rng.x1 = *reinterpret_cast<const uint32_t *>(rng_slot + 256u + so);
@@ -2362,10 +2367,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
   }
 
-  if (A.span && lane == 0) {   // vector atomics from one lane per wave: first start, last end of the launch
-    atomicMax(A.span, static_cast<unsigned long long>(~t_wave0));
+  if (A.span && lane == 0)   // vector atomics from one lane per wave: first start (above), last end of the launch
     atomicMax(A.span + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
-  }
   if (TRACE && A.wave_trace && lane == 0) {
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
     const uint32_t hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));     // HW_REG_HW_ID
