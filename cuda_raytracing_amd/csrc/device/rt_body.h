@@ -9,6 +9,10 @@
 // Arithmetic is the reference's, op for op: built with -ffp-contract=off and correctly rounded f32
 // divide/sqrt, ternary MIN/MAX semantics, the same RNG draw order — bit-exact against the oracle.
 #pragma once
+// RT_PRIM_LISTS=0 (RT_JIT_OPTS=-DRT_PRIM_LISTS=0) compiles the verified walk without the camera-ray list path (A/B)
+#ifndef RT_PRIM_LISTS
+#define RT_PRIM_LISTS 1
+#endif
 #include "rt_layout.h"
 
 #ifndef RT_UNWIND_BATCH
@@ -965,7 +969,7 @@ struct AccelTraceK {
       // the ray could accept gives the same record ((1) above), and a sphere whose lower bound lies beyond the
       // ray's axial reach below tmax (|o - centre| + tmax |d|, rounded up) cannot yield a root below tmax, nor
       // can any later one; the reach proof and the fallback below apply unchanged
-      if (!resume && T.atie != 0u) {
+      if (RT_PRIM_LISTS && !resume && T.atie != 0u) {
         const uint32_t tile = T.atie - 1u;
         const uint32_t n = A.prim_counts[tile];
         const uint32_t cap = A.prim_cap;
@@ -2110,7 +2114,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 
     // ---- trace one path segment per busy lane (hit(), :1340) ----
     const bool tracing = busy && !pending;   // a lane still resuming its rejection keeps its hit
-    if constexpr (prim_lists<Trace>(0)) {
+    if constexpr (RT_PRIM_LISTS && prim_lists<Trace>(0)) {
       // a camera ray (no bounce yet, no paused walk) of a shard with candidate lists: its tile's list
       T.atie = 0u;
       if (A.prim_lists && tracing && depth == 0u && !T.active) {
