@@ -1184,7 +1184,8 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     rt::SphereAccel a;
     std::string why;
     if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
-    src = rt::jit_accel_source(img, variant, rt::accel_waves(), rt::accel_width() == 4 ? (rt::accel_quant() ? 2 : 1) : 0);
+    const int wide = rt::accel_width() == 4 ? (rt::accel_quant() ? 2 : 1) : 0;
+    src = rt::jit_accel_source(img, variant, rt::accel_waves(wide), wide);
   } else if (traversal == RT_TRAV_MIXED) {
     rt::MixedAccel m;
     std::string why;

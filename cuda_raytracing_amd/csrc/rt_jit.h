@@ -41,7 +41,7 @@ bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels 
 std::string jit_accel_source(const SceneImage &img, int variant, int waves = 0, int wide = 0);   // waves > 0: amdgpu_waves_per_eu
 int accel_width();   // 2 or 4 (RT_ACCEL_WIDTH)
 bool accel_quant();  // the 4-wide tree quantised (RT_ACCEL_QUANT, default off)
-int accel_waves();   // the verified sphere walk's waves per SIMD request (6; RT_ACCEL_WAVES, 0 = allocator's choice)
+int accel_waves(int wide = 0);   // the verified walk's waves per SIMD request (6, 4-wide 5; RT_ACCEL_WAVES, 0 = allocator's choice)
 // verified mixed-world traversal kernels (MixedTraceK over the scene's node kinds)
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why);
 std::string jit_mixed_source(const SceneImage &img, int variant, int waves = 0);
