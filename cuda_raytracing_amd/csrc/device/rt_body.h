@@ -1880,8 +1880,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   uint32_t chunk_pos = 0, chunk_end = 0;   // wave-uniform: ids of the wave's current tile
   // the wave's slot: a wave-uniform base (scalar registers; threadIdx.x >> 6 is not known to be uniform) and
   // 32-bit per-lane offsets
-  char *const rng_slot = reinterpret_cast<char *>(A.rng_slot) +
-                         static_cast<size_t>(__builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + wave)) * kRngSlotWords * 4u;
+  // the wave's RNG slot in LDS (32-bit words, one per lane and state word)
+  uint32_t *const rng_slot = g_lds + A.rng_slot_word + wave * kRngSlotWords;
   bool exhausted = false;
   bool prio_done = false;                  // wave-uniform: the split costliest tiles are all handed out
   uint32_t tiles_taken = 0, rounds = 0;
@@ -2018,12 +2018,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           rng_jump_nib(rs, tcol * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
           // slot entry id & 63: a chunk is size-aligned (whole tiles, or prio_chunk pieces, a power of two <= 64),
           // so its ids take distinct entries and no chunk base is kept across rounds
-          const uint32_t so = (id & 63u) * 4u;
-          *reinterpret_cast<uint32_t *>(rng_slot + so) = x0;
-          *reinterpret_cast<uint32_t *>(rng_slot + 256u + so) = x1;
-          *reinterpret_cast<uint32_t *>(rng_slot + 512u + so) = x2;
-          *reinterpret_cast<uint32_t *>(rng_slot + 768u + so) = x3;
-          *reinterpret_cast<uint32_t *>(rng_slot + 1024u + so) = x4;
+          const uint32_t so = id & 63u;
+          rng_slot[so] = x0;
+          rng_slot[64u + so] = x1;
+          rng_slot[128u + so] = x2;
+          rng_slot[192u + so] = x3;
+          rng_slot[256u + so] = x4;
           __threadfence_block();   // the stores reach the wave's later loads of other lanes' entries
         }
       }
@@ -2059,13 +2059,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
           } else {
             // the state seeded at the chunk's pickup (the slot entry of this id)
-            const uint32_t so = (id & 63u) * 4u;
+            const uint32_t so = id & 63u;
             rng.d = A.rng_d;
-            rng.x0 = *reinterpret_cast<const uint32_t *>(rng_slot + so);
-            rng.x1 = *reinterpret_cast<const uint32_t *>(rng_slot + 256u + so);
-            rng.x2 = *reinterpret_cast<const uint32_t *>(rng_slot + 512u + so);
-            rng.x3 = *reinterpret_cast<const uint32_t *>(rng_slot + 768u + so);
-            rng.x4 = *reinterpret_cast<const uint32_t *>(rng_slot + 1024u + so);
+            rng.x0 = rng_slot[so];
+            rng.x1 = rng_slot[64u + so];
+            rng.x2 = rng_slot[128u + so];
+            rng.x3 = rng_slot[192u + so];
+            rng.x4 = rng_slot[256u + so];
           }
           sum = mk(0, 0, 0);
           sample = 0;

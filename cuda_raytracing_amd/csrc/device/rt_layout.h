@@ -202,7 +202,8 @@ struct RenderArgs {
   const uint32_t *rng_rows;   // [rows][8 columns][8] phase bases {x0..x4, pad}: pixel (lr, c), c < 8
   const uint32_t *rng_nib;    // [tiles_x][kRngNibTableWords]: nibble table of J^(8 t) for tile column t
   uint32_t rng_d;             // the Weyl word d (the same for every subsequence)
-  uint32_t *rng_slot;         // per wave [5][64]: the states of the chunk of pixel ids it took last
+  uint32_t rng_slot_word;     // LDS word of the block's per-wave slots, [wave][5][64]: the states of the chunk of pixel
+                              // ids the wave took last (kRngSlotWords per wave)
   float *out;                 // [n_pixels][3]
   uint8_t *out8;              // optional [n_pixels][3] P6 payload bytes (pixels_to_ppm), null = none
   void *rc;                   // colour-stack levels past the LDS ones: [threads][max_bounces] codes

@@ -75,6 +75,7 @@ constexpr uint32_t kPrimMinSpheres = 2048;  // primary-ray candidate lists by de
 constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
+constexpr size_t kRngSlotBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kRngSlotWords * 4;   // per block, LDS
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
@@ -172,7 +173,7 @@ struct rt_context {
   uint32_t mix_nodes = 0, mix_prims = 0;
   bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
   int static_ok = -1;          // the scene expands within jit_budget (straight-line, stackless traversal); -1 unknown
-  DevBuf scene, jump, rng_rows, rng_cols, rng_slot, rc, work, counters, wave_trace, tile_cost, tile_order, prim_lists, prim_counts;
+  DevBuf scene, jump, rng_rows, rng_cols, rc, work, counters, wave_trace, tile_cost, tile_order, prim_lists, prim_counts;
   // seeding tables of the last geometry, kept on the device: the phase bases (xorwow_phase_bases; key = seed, W,
   // rows of the shard) and the column tables (xorwow_column_tables; key = W)
   uint64_t rows_key[5] = {~0ull, 0, 0, 0, 0};
@@ -374,7 +375,7 @@ void rt_context_destroy(rt_context *c) {
   {
     DeviceGuard g(c->device);
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
-    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->prim_lists.release(); c->prim_counts.release(); c->rng_slot.release(); c->rc.release();
+    c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->prim_lists.release(); c->prim_counts.release(); c->rc.release();
     c->work.release(); c->counters.release();
     c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
   }
@@ -593,8 +594,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const uint32_t stack_cap = std::max({c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u,
                                        c->accel_w4 ? c->accel.wide_stack : 0u,
                                        c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u});
-  const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2;
-  size_t stack_bytes = stackless ? 0 : full_stack_bytes;
+  // (+ the block's RNG slots, kRngSlotBytes: the "stack" region's fixed tail)
+  const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2 + kRngSlotBytes;
+  size_t stack_bytes = stackless ? kRngSlotBytes : full_stack_bytes;
   // one block may declare at most the CU's 160 KiB: a deep per-lane stack first evicts the LDS copy of
   // the scene (read from HBM instead); if the stack and the minimum colour-stack levels alone do not
   // fit, the scene is too deep for this kernel (a status, not a failed launch)
@@ -611,7 +613,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const uint32_t cb_jit = byte_ok ? 1u : (narrow_ok ? 2u : 4u);
   const size_t lds_only_need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb_jit) +
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
-                               (stackless ? 0 : full_stack_bytes) + kLdsReserve;
+                               (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
   const bool rc_lds_only = c->rc_lds_auto && lds_only_need <= kLdsPerCu / 8;
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
@@ -700,7 +702,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     }
   }
   if (trav == RT_TRAV_PACKET) c->variant |= rt::kVarPacket;
-  if (jit_fn && !jit_lane) stack_bytes = 0;   // straight-line traversal: no stacks
+  if (jit_fn && !jit_lane) stack_bytes = kRngSlotBytes;   // straight-line traversal: no stacks (the RNG slots stay)
   // the verified walk's top nodes staged in LDS (breadth-first prefix of the SAH tree) where the scene
   // itself is not: they take the scene's place at the start of the block's LDS
   uint32_t accel_lds_nodes = 0;
@@ -790,7 +792,6 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
       c->cols_width = p->width;
     }
   }
-  if (c->rng_slot.ensure(static_cast<size_t>(threads / 64) * rt::kRngSlotWords * 4) != hipSuccess) return RT_ERR_HIP;
   if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;   // (wide codes' size)
   c->used_rc_levels = rc_levels;
   c->rc_audit_bytes = 0;
@@ -846,7 +847,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.rng_rows = static_cast<const uint32_t *>(c->rng_rows.p);
   a.rng_nib = static_cast<const uint32_t *>(c->rng_cols.p);
   a.rng_d = seed_base[0];
-  a.rng_slot = static_cast<uint32_t *>(c->rng_slot.p);
+  a.rng_slot_word = scene_lds_words + rc_lds_words + static_cast<uint32_t>((stack_bytes - kRngSlotBytes) / 4);
   a.out = out_dev;
   a.out8 = out8_dev;
   a.rc = c->rc.p;
@@ -933,7 +934,6 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     pa.out = nullptr;
     pa.out8 = nullptr;
     pa.rng_rows = nullptr;
-    pa.rng_slot = nullptr;
     pa.work = static_cast<uint32_t *>(c->work.p) + 8;
     pa.wave_trace = nullptr;
     pa.fold_violation = static_cast<uint32_t *>(c->work.p) + 14;   // probe rays: flag ignored
@@ -1173,7 +1173,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
   {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks)
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
     const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +
-                        (img.words.size() <= rt::kLdsSceneMaxWords ? img.words.size() * 4 : 4096u) + kLdsReserve;
+                        (img.words.size() <= rt::kLdsSceneMaxWords ? img.words.size() * 4 : 4096u) + kRngSlotBytes + kLdsReserve;
     if (traversal == RT_TRAV_STATIC && need <= kLdsPerCu / 8) variant |= rt::kVarRcLds;
   }
   std::string src;
