@@ -76,6 +76,7 @@ constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr size_t kRngSlotBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kRngSlotWords * 4;   // per block, LDS
+constexpr size_t kRcLdsOnlyBlocks = 6;   // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
@@ -608,13 +609,15 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + rc_bytes + stack_bytes;
   c->variant = (c->lds ? rt::kVarLds : 0) | (c->counted ? rt::kVarCount : 0) |
                (c->img.has_noise ? rt::kVarNoise : 0) | (c->img.needs_uv ? rt::kVarUv : 0);
-  // every colour-stack level of a run-time kernel in LDS at ANY residency (8 blocks/CU), scene staging and per-lane
-  // stacks included: such kernels carry no HBM level code (kVarRcLds).  Set below only when the levels are kept.
+  // every colour-stack level of a run-time kernel in LDS at 6 blocks/CU (the residency of every run-time render kernel
+  // measured: 77-169 VGPRs; one that would reach 7-8 loses that step to LDS, never correctness), scene staging, per-lane
+  // stacks and RNG slots included: such kernels carry no HBM level code (kVarRcLds).  Set below only when the levels
+  // are kept.
   const uint32_t cb_jit = byte_ok ? 1u : (narrow_ok ? 2u : 4u);
   const size_t lds_only_need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb_jit) +
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
-  const bool rc_lds_only = c->rc_lds_auto && lds_only_need <= kLdsPerCu / 8;
+  const bool rc_lds_only = c->rc_lds_auto && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
@@ -1174,7 +1177,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
     const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +
                         (img.words.size() <= rt::kLdsSceneMaxWords ? img.words.size() * 4 : 4096u) + kRngSlotBytes + kLdsReserve;
-    if (traversal == RT_TRAV_STATIC && need <= kLdsPerCu / 8) variant |= rt::kVarRcLds;
+    if (traversal == RT_TRAV_STATIC && need <= kLdsPerCu / kRcLdsOnlyBlocks) variant |= rt::kVarRcLds;
   }
   std::string src;
   if (traversal == RT_TRAV_STATIC) {
