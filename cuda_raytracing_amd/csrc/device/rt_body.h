@@ -1796,9 +1796,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const bool probe = (F & kVarProbe) != 0 || ((F & kVarNoProbe) == 0 && A.probe_cost != nullptr);
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
-  // kernel-only span (A.span): the first wave's start is recorded at once (no 64-bit value held to the end)
-  if (A.span && __lane_id() == 0)
-    atomicMax(A.span, static_cast<unsigned long long>(~__builtin_amdgcn_s_memrealtime()));
+  // kernel-only span (A.span): the start is block 0's first wave (blocks are dispatched in order; a start atomic
+  // from every wave serialised ~6k same-address device atomics ahead of the first barrier: scene 0 +8 ms,
+  // profiles/r04_ab_v17_scene0.jsonl), recorded at once rather than held in registers to the end
+  if (A.span && blockIdx.x == 0 && threadIdx.x == 0)
+    A.span[0] = static_cast<unsigned long long>(~__builtin_amdgcn_s_memrealtime());
   Mem<LDS> S{A.scene};
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
