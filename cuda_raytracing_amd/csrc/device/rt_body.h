@@ -1908,6 +1908,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
              add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
                  scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
   };
+  // kernels with register room (every trace but the verified sphere walk, whose 6-wave build is at its 80-VGPR
+  // budget) keep the point from the pixel's pickup instead of recomputing it for every sample
+  constexpr bool kCarryPoint = !lazy_hit<Trace>(0);
+  f3 pp = mk(0, 0, 0);
   auto camera_ray = [&]() {                                                 // :1561-1578
     if (A.defocus_angle <= 0) {
       ray.o = mk(A.center[0], A.center[1], A.center[2]);
@@ -1925,7 +1929,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
     float xo = rng.uniform() - 0.5f;
     float yo = rng.uniform() - 0.5f;
-    ray.d = sub(pixel_point(), ray.o);
+    ray.d = sub(kCarryPoint ? pp : pixel_point(), ray.o);
     ray.d = add(ray.d, scale(xo, mk(A.du[0], A.du[1], A.du[2])));
     ray.d = add(ray.d, scale(yo, mk(A.dv[0], A.dv[1], A.dv[2])));
     ray.time = rng.uniform();
@@ -2049,6 +2053,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         const uint32_t lr = ty * 8 + (k >> 3), j = tx * 8 + (k & 7u);
         if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
           pxy = (lr << 16) | j;
+          if constexpr (kCarryPoint) pp = pixel_point();
           need = false;
           busy = true;
           hot = id < A.prio_ids;
