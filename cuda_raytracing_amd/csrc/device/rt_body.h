@@ -1228,6 +1228,8 @@ struct AccelTraceK {
 // Traces whose hit record is rebuilt at shading time (kLazyHit) — detected without <type_traits> (hipRTC)
 template <class TR> __device__ constexpr auto lazy_hit(int) -> decltype(TR::kLazyHit, bool()) { return TR::kLazyHit; }
 template <class TR> __device__ constexpr bool lazy_hit(long) { return false; }
+template <class TR> __device__ constexpr auto carry_point(int) -> decltype(TR::kCarryPoint, bool()) { return TR::kCarryPoint; }
+template <class TR> __device__ constexpr bool carry_point(long) { return false; }
 template <class TR> __device__ constexpr auto prim_lists(int) -> decltype(TR::kPrimLists, bool()) { return TR::kPrimLists; }
 template <class TR> __device__ constexpr bool prim_lists(long) { return false; }
 
@@ -1908,9 +1910,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
              add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
                  scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
   };
-  // kernels with register room (every trace but the verified sphere walk, whose 6-wave build is at its 80-VGPR
-  // budget) keep the point from the pixel's pickup instead of recomputing it for every sample
-  constexpr bool kCarryPoint = !lazy_hit<Trace>(0);
+  // the scene-specialised kernels (register room at 72-85 VGPRs) keep the point from the pixel's pickup instead of
+  // recomputing it for every sample; the walks at a register budget (the verified sphere walk's 80, the mixed
+  // walk's 160) recompute it (a few ops, no division)
+  constexpr bool kCarryPoint = carry_point<Trace>(0);
   f3 pp = mk(0, 0, 0);
   auto camera_ray = [&]() {                                                 // :1561-1578
     if (A.defocus_angle <= 0) {

@@ -374,6 +374,7 @@ bool generate_static_trace(const SceneImage &img, uint32_t max_visits, bool fold
   if (!g.ok) return false;
   src->clear();
   *src += "struct StaticTrace {\n";
+  *src += "  static constexpr bool kCarryPoint = true;   // render_body keeps the viewport point per pixel\n";
   *src += "  template <bool LDS, bool COUNT, bool UV>\n";
   *src += "  __device__ __forceinline__ static void run(const Mem<LDS> &, const RenderArgs &A, bool busy, uint64_t,\n";
   *src += "                                             uint32_t, uint16_t *, Trav &T, Ray &r, Hit &h, Visits &vc) {\n";
