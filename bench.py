@@ -270,6 +270,41 @@ def load_traffic(workload: str, key: str = "bytes"):
         return None
 
 
+def launch_plan(gpus: int, env, device_count: int, backend: str = "nccl"):
+    """How `bench.py --gpus N` runs: ("run", None) in this process, ("spawn", n) = start n rank processes (no
+    launcher set WORLD_SIZE and N > 1), or ("error", message).  Decided before the first GPU call: counting
+    devices does not initialise the GPU.  The reference renders on one device (raytracing.cu:1649-1773); N ranks
+    take interleaved rows (multi_gpu.py) and are one process per GPU, so N ranks need N devices — except the gloo
+    rehearsal, which may share one device between ranks."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if gpus <= 1:
+            return "run", None
+        if device_count < gpus:
+            return "error", (f"--gpus {gpus} needs {gpus} GPUs (one rank per GPU) but {device_count} "
+                             f"{'is' if device_count == 1 else 'are'} visible; refusing to report a smaller run")
+        return "spawn", gpus
+    world = int(ws)
+    if world != gpus:
+        return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+    if world > 1 and backend == "nccl" and device_count < world:
+        return "error", f"WORLD_SIZE={world} ranks over RCCL need {world} GPUs, {device_count} visible"
+    return "run", None
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """--gpus N without a launcher: run this script as N ranks under torch.distributed.run (one process per GPU,
+    rendezvous on 127.0.0.1), as a child process; returns its exit code.  This process has not touched the GPU."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+    log("launching: " + " ".join(cmd))
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -290,11 +325,15 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (plumbing rehearsal)")
     args = ap.parse_args()
 
+    plan, what = launch_plan(args.gpus, os.environ, torch.cuda.device_count(), args.dist_backend)
+    if plan == "error":
+        log(f"bench.py: {what}")
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(what, sys.argv[1:]))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world_size}; using WORLD_SIZE")
     dev = local_rank % max(torch.cuda.device_count(), 1)   # == local_rank on a node with a GPU per rank
     torch.cuda.set_device(dev)
     if world_size > 1:
@@ -397,6 +436,12 @@ def main():
     med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
     render_ms = med([st.render_kernel_ms if st.render_kernel_ms > 0 else st.render_ms for st in fstats])
     render_event_ms = med([st.render_ms for st in fstats])
+    # frames run one after the other on one stream, so the timed frames' kernel spans cannot add up to more
+    # than the timed wall time: mean span <= mean step (a span above it would be a timing defect)
+    spans = [st.render_kernel_ms if st.render_kernel_ms > 0 else st.render_ms for st in fstats]
+    render_mean_ms = sum(spans) / len(spans)
+    step_mean_ms = elapsed / args.steps * 1e3
+    assert render_mean_ms <= step_mean_ms, f"mean render span {render_mean_ms:.3f} ms > mean step {step_mean_ms:.3f} ms"
     seed_ms = med([st.init_ms for st in fstats])
     sched_ms = med([st.sched_ms for st in fstats])
     achieved = ops_per_sample * local_samples / (render_ms / 1e3) / 1e12
@@ -463,7 +508,8 @@ def main():
                            rt.RT_TRAV_MIXED: "rt_mixed_render (hipRTC)"}.get(
                     cst.traversal, "rt_lane_render (hipRTC)"),
             },
-            "kernel_ms": {"render_median": round(render_ms, 3), "render_event_median": round(render_event_ms, 3),
+            "kernel_ms": {"render_median": round(render_ms, 3), "render_mean": round(render_mean_ms, 3),
+                          "render_event_median": round(render_event_ms, 3),
                           "seed_median": round(seed_ms, 3),
                           "schedule_median": round(sched_ms, 3),
                           "render_only_msamples_s": round(local_samples / (render_ms / 1e3) / 1e6, 1)},

@@ -2134,6 +2134,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     Trace::template run<LDS, COUNT, UV>(S, A, tracing, __ballot(tracing), lane, stk, T, ray, h, vc);
     if (T.active) continue;                   // walk paused (verified traversal): resumes next round
     if constexpr (lazy_hit<Trace>(0)) Trace::template materialize<LDS, UV>(S, A, T, ray, h);
+#ifdef RT_DBG_PX   // diagnostics only (RT_JIT_OPTS=-DRT_DBG_PX=<row << 16 | column>): one pixel's path segments
+    if (tracing && pxy == static_cast<uint32_t>(RT_DBG_PX))
+      printf("dbg s %d d %u res %d t %08x best %08x o %08x %08x %08x dir %08x %08x %08x rng %08x\n", sample, depth,
+             T.result ? 1 : 0, __float_as_uint(T.tmax), T.abest, __float_as_uint(ray.o.x), __float_as_uint(ray.o.y),
+             __float_as_uint(ray.o.z), __float_as_uint(ray.d.x), __float_as_uint(ray.d.y), __float_as_uint(ray.d.z), rng.x4);
+#endif
     if (TRACE) {
       const uint64_t t = __builtin_amdgcn_s_memtime();
       ph_trace += t - t_mark; if (lone) lph[1] += t - t_mark;

@@ -40,6 +40,39 @@ struct DevBuf {
   void release() { if (p) (void)hipFree(p); p = nullptr; bytes = 0; }
 };
 
+// Pinned host staging for the per-geometry seeding tables, uploaded with hipMemcpyAsync on the frame's stream (the
+// copy is ordered after the previous frame's render on that stream, which may still read the old table); `done`
+// marks the copy's completion so the staging bytes are not rewritten while a copy from them is pending
+struct PinBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t done = nullptr;
+  bool pending = false;
+  hipError_t stage(const void *src, size_t n) {
+    if (pending) {
+      if (hipEventSynchronize(done) != hipSuccess) return hipErrorUnknown;
+      pending = false;
+    }
+    if (n > bytes) {
+      if (p) (void)hipHostFree(p);
+      p = nullptr;
+      bytes = 0;
+      const hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+      if (e != hipSuccess) return e;
+      bytes = n;
+    }
+    if (!done && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) return hipErrorUnknown;
+    std::memcpy(p, src, n);
+    return hipSuccess;
+  }
+  void release() {
+    if (pending && done) (void)hipEventSynchronize(done);
+    if (p) (void)hipHostFree(p);
+    if (done) (void)hipEventDestroy(done);
+    p = nullptr; bytes = 0; done = nullptr; pending = false;
+  }
+};
+
 struct DeviceGuard {   // restore the caller's current device
   int prev = -1;
   explicit DeviceGuard(int dev) { if (hipGetDevice(&prev) != hipSuccess) prev = -1; (void)hipSetDevice(dev); }
@@ -179,6 +212,8 @@ struct rt_context {
   // rows of the shard) and the column tables (xorwow_column_tables; key = W)
   uint64_t rows_key[5] = {~0ull, 0, 0, 0, 0};
   int cols_width = -1;
+  PinBuf rows_stage, cols_stage;   // their pinned staging (stream-ordered uploads)
+  bool ev_recorded = false;        // ev[2] has been recorded (a frame was enqueued before)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
   bool lds = false;
   bool counted = false;
@@ -229,6 +264,7 @@ struct rt_context {
   size_t rc_audit_bytes = 0;      // RT_FLAG_RC_AUDIT: bytes of the HBM colour-stack buffer filled before the render
   uint32_t rc_audit_code = 4;     // ... holding codes of this many bytes
   bool rc_no_byte = false;        // RT_RC_BYTE=0: 16-bit codes where 8-bit ones would do (A/B)
+  bool rc_lds_only_off = false;   // set while a render is redone without kVarRcLds (its layout did not fit)
   uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
   double jit_ms = 0.0;            // ... and the host time spent obtaining them
@@ -379,6 +415,7 @@ void rt_context_destroy(rt_context *c) {
     c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->prim_lists.release(); c->prim_counts.release(); c->rc.release();
     c->work.release(); c->counters.release();
     c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
+    c->rows_stage.release(); c->cols_stage.release();
   }
   delete c;
 }
@@ -546,6 +583,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (n == 0) {   // same event order as a render: seed | schedule | render, ev[2] (render end) last
     for (int k : {0, 1, 3, 2})
       if (hipEventRecord(c->ev[k], s) != hipSuccess) return RT_ERR_HIP;
+    c->ev_recorded = true;
     c->rendered = true;
     return RT_OK;
   }
@@ -556,6 +594,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     if (hipMemsetAsync(out_dev, 0, static_cast<size_t>(n) * 12, s) != hipSuccess) return RT_ERR_HIP;
     if (out8_dev && hipMemsetAsync(out8_dev, 0, static_cast<size_t>(n) * 3, s) != hipSuccess) return RT_ERR_HIP;
     if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
+    c->ev_recorded = true;
     c->rendered = true;
     return RT_OK;
   }
@@ -617,7 +656,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const size_t lds_only_need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb_jit) +
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
-  const bool rc_lds_only = c->rc_lds_auto && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
+  const bool rc_lds_only = c->rc_lds_auto && !c->rc_lds_only_off && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
@@ -747,7 +786,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
       uint32_t lv = std::min<uint32_t>(mb, std::min<uint32_t>(kRcLdsMaxLevels, std::max(fit, rc_levels)));
       lv = std::max<uint32_t>(lv / codes_per_word * codes_per_word, rc_levels);   // whole words (rc_levels already is)
       // a kernel without HBM levels (kVarRcLds) holds every level: mb rounded up to whole words (the host check
-      // above guarantees they fit at 8 blocks/CU)
+      // above predicts they fit at kRcLdsOnlyBlocks = 6 blocks/CU; verified below once the layout is final)
       if (lds_only_kernel) lv = (mb + codes_per_word - 1) / codes_per_word * codes_per_word;
       if (lv > rc_levels || lds_only_kernel) {
         const size_t lds2 = fixed + lv * level_bytes;
@@ -759,6 +798,25 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
         }
       }
     }
+  }
+  if (lds_only_kernel) {
+    // The kVarRcLds decision was made on a predicted layout (before the kernels were built: straight-line stackless
+    // traversal, 4 KiB of staged SAH nodes).  The kernel stores every level in LDS, so the final layout must hold all
+    // mb levels within one block's LDS, or the render is made again without that variant (nothing is enqueued yet);
+    // residency is then whatever that layout allows (the grid never exceeds the resident blocks).
+    const uint32_t need_levels = (mb + codes_per_word - 1) / codes_per_word * codes_per_word;
+    if (rc_levels < need_levels || c->lds_bytes + kLdsReserve > kLdsPerCu) {
+      if (std::getenv("RT_DEBUG"))
+        std::fprintf(stderr, "[rt] LDS-only colour stack does not fit (%u of %u levels, %zu B): rebuilding with HBM levels\n",
+                     rc_levels, need_levels, c->lds_bytes);
+      c->rc_lds_only_off = true;
+      const int r = rt_context_render_ppm(c, cam, p, out_dev, out8_dev, stream);
+      c->rc_lds_only_off = false;
+      return r;
+    }
+    int per_cu_lds = rt::jit_blocks_per_cu(jit_fn, c->lds_bytes);
+    if (c->blocks_per_cu > 0) per_cu_lds = std::min(c->blocks_per_cu, per_cu_lds);
+    per_cu = std::min(per_cu, per_cu_lds);
   }
   const uint32_t rc_lds_words = static_cast<uint32_t>(rc_levels * level_bytes / 4);
   uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
@@ -775,23 +833,34 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // RNG: the phase bases of this shard's rows and the column tables (host, once per geometry: a few ms; the
   // per-pixel jumps — one nibble-table product each — run in the render kernel at tile pickup) and the per-wave
   // slots
+  // The tables are rewritten in place when the geometry changes, so the upload is stream-ordered: an async copy on
+  // the frame's stream from pinned staging, after the previous frame's render (the same stream, or — a caller
+  // alternating streams on one context — its render-end event), so a frame still in flight keeps reading the
+  // table it was launched with (a blocking null-stream copy did not wait for non-blocking streams).
   {
     const uint64_t key[5] = {p->seed, static_cast<uint64_t>(p->width), static_cast<uint64_t>(p->row_offset),
                              static_cast<uint64_t>(p->row_stride), static_cast<uint64_t>(p->row_count)};
-    if (std::memcmp(key, c->rows_key, sizeof key) != 0) {
+    const bool rows_new = std::memcmp(key, c->rows_key, sizeof key) != 0, cols_new = c->cols_width != p->width;
+    if ((rows_new || cols_new) && c->ev_recorded && hipStreamWaitEvent(s, c->ev[2], 0) != hipSuccess) return RT_ERR_HIP;
+    auto upload = [s](DevBuf &dst, PinBuf &stage, const std::vector<uint32_t> &v) {
+      const size_t n = v.size() * 4;
+      if (dst.ensure(n) != hipSuccess || stage.stage(v.data(), n) != hipSuccess ||
+          hipMemcpyAsync(dst.p, stage.p, n, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipEventRecord(stage.done, s) != hipSuccess)
+        return false;
+      stage.pending = true;
+      return true;
+    };
+    if (rows_new) {
       std::vector<uint32_t> rb;
       rt::xorwow_phase_bases(p->seed, p->width, p->row_offset, p->row_stride, p->row_count, &rb);
-      if (c->rng_rows.ensure(rb.size() * 4) != hipSuccess ||
-          hipMemcpy(c->rng_rows.p, rb.data(), rb.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-        return RT_ERR_HIP;
+      if (!upload(c->rng_rows, c->rows_stage, rb)) return RT_ERR_HIP;
       std::memcpy(c->rows_key, key, sizeof key);
     }
-    if (c->cols_width != p->width) {
+    if (cols_new) {
       std::vector<uint32_t> ct;
       rt::xorwow_column_tables(p->width, &ct);
-      if (c->rng_cols.ensure(ct.size() * 4) != hipSuccess ||
-          hipMemcpy(c->rng_cols.p, ct.data(), ct.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-        return RT_ERR_HIP;
+      if (!upload(c->rng_cols, c->cols_stage, ct)) return RT_ERR_HIP;
       c->cols_width = p->width;
     }
   }
@@ -988,6 +1057,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
   if (le != hipSuccess) return RT_ERR_HIP;
   if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
+  c->ev_recorded = true;
   c->last_cam = *cam;
   c->last_params = *p;
   c->last_out = out_dev;

@@ -1,9 +1,10 @@
 """Row-interleaved frame sharding over ranks + one gather to rank 0.
 
 Pixels are independent and each pixel's RNG subsequence is its GLOBAL index, so a frame splits by
-rows with no exchange during rendering; the only collective is one gather of each shard's float32
-RGB rows to rank 0 at the end of the frame (RCCL over xGMI with the "nccl" backend on GPUs, gloo in
-the CPU tests), followed by a row un-permute on rank 0.  This is not a translation of any reference
+rows with no exchange during rendering; the only collective is one gather of each shard's rows to
+rank 0 at the end of the frame (RCCL over xGMI with the "nccl" backend on GPUs, gloo in the CPU tests),
+followed by a row un-permute on rank 0.  gather_rows moves whatever dtype it is given: bench.py gathers
+the u8 PPM bytes the render kernel writes (3 B/pixel), the tests gather float32 frames too.  This is not a translation of any reference
 collective: the reference is single-GPU.
 """
 from __future__ import annotations
@@ -34,7 +35,8 @@ def gather_rows(local: torch.Tensor, height: int, width: int, rank: int, world: 
     """Gather row-interleaved shards [rows_r, W, 3] onto rank 0 and assemble [H, W, 3].
 
     Shards are padded to ceil(H/world) rows so one fixed-size gather moves everything
-    (per-rank message = ceil(H/G) * W * 12 bytes: 3.1 MB at 1080p/8 GPUs)."""
+    (per-rank message = ceil(H/G) * W * 3 * itemsize bytes: 0.78 MB of u8 PPM bytes at 1080p/8 GPUs,
+    3.1 MB of float32)."""
     rows = max_shard_rows(height, world)
     if local.shape[0] != rows:
         pad = torch.zeros((rows - local.shape[0], width, 3), dtype=local.dtype, device=local.device)
