@@ -179,7 +179,7 @@ HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_contex
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
                "rt_seed_states", "rt_kernel_source", "rt_mixed_build", "rt_multi_create", "rt_multi_render",
                "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map", "rt_accel_build_wide", "rt_rng_table_states",
-               "rt_accel_build_quant", "rt_prim_lists"]
+               "rt_accel_build_quant", "rt_prim_lists", "rt_multi_unpermute"]
 
 
 def _bind_single_hip_runtime():
@@ -243,6 +243,7 @@ def hip_lib():
             C.c_int, P, P, C.POINTER(Stats))
         i32p = C.POINTER(C.c_int32)
         opt("rt_multi_row_map", C.c_int, C.c_int32, C.c_int32, C.c_int32, i32p, i32p, i32p, i32p)
+        opt("rt_multi_unpermute", C.c_int, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_uint32, P)
         _hip = L
     return _hip
 

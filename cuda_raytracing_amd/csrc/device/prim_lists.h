@@ -1,6 +1,6 @@
 // prim_lists.h — primary-ray candidate lists of the verified sphere walk (host and device).
 //
-// Every camera ray of an 8x8 tile (raytracing.cu:1561-1578: origin in the defocus disc around the camera centre C,
+// Every camera ray of a 64-pixel tile (raytracing.cu:1561-1578: origin in the defocus disc around the camera centre C,
 // direction = the pixel sample point P on the focus plane - origin, P within half a pixel of the pixel centre) lies
 // in the cone  K = union over t >= 0 of Ball(C + t a, rho + t w),  a = the tile footprint's centre Qc - C,
 // w = rho + hq, where rho bounds |origin - C| and hq bounds |P - Qc| over the footprint (both widened for the
@@ -32,6 +32,7 @@ struct PrimListGeom {
   double half_motion;                  // max over spheres of |motion| / 2 (0: none moves)
   int32_t width, rows, row_offset, row_stride;
   uint32_t tiles_x;
+  uint32_t tile_shift;                 // tiles of 64 pixels, 1 << tile_shift wide (RenderArgs::tile_shift)
 };
 
 constexpr uint32_t kPrimListNone = 0xffffffffu;   // count of a tile without a list (overflow / degenerate cone)
@@ -50,8 +51,9 @@ struct PrimCone {
 // the cone of tile `tile` of the shard; false: no list (past the shard, degenerate or wide cone)
 __host__ __device__ inline bool prim_cone(const PrimListGeom &g, uint32_t tile, PrimCone *k) {
   const uint32_t ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
-  const int32_t lr0 = static_cast<int32_t>(ty) * 8, lr1 = lr0 + 7 < g.rows - 1 ? lr0 + 7 : g.rows - 1;
-  const int32_t j0 = static_cast<int32_t>(tx) * 8, j1 = j0 + 7 < g.width - 1 ? j0 + 7 : g.width - 1;
+  const int32_t tw = 1 << g.tile_shift, th = 64 >> g.tile_shift;
+  const int32_t lr0 = static_cast<int32_t>(ty) * th, lr1 = lr0 + th - 1 < g.rows - 1 ? lr0 + th - 1 : g.rows - 1;
+  const int32_t j0 = static_cast<int32_t>(tx) * tw, j1 = j0 + tw - 1 < g.width - 1 ? j0 + tw - 1 : g.width - 1;
   if (lr0 >= g.rows || j0 >= g.width) return false;
   const double y0 = g.row_offset + static_cast<double>(lr0) * g.row_stride - 0.5;
   const double y1 = g.row_offset + static_cast<double>(lr1) * g.row_stride + 0.5;

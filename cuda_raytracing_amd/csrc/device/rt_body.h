@@ -1798,11 +1798,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const bool probe = (F & kVarProbe) != 0 || ((F & kVarNoProbe) == 0 && A.probe_cost != nullptr);
   constexpr uint32_t MM = ((F >> kVarMatShift) & 15) ? ((F >> kVarMatShift) & 15) : 15u;   // material kinds
   constexpr uint32_t TM = ((F >> kVarTexShift) & 15) ? ((F >> kVarTexShift) & 15) : 15u;   // texture kinds
-  // kernel-only span (A.span): the start is block 0's first wave (blocks are dispatched in order; a start atomic
-  // from every wave serialised ~6k same-address device atomics ahead of the first barrier: scene 0 +8 ms,
-  // profiles/r04_ab_v17_scene0.jsonl), recorded at once rather than held in registers to the end
-  if (A.span && blockIdx.x == 0 && threadIdx.x == 0)
-    A.span[0] = static_cast<unsigned long long>(~__builtin_amdgcn_s_memrealtime());
+  // kernel-only span (A.span): the start is the earliest first wave of blocks 0..7 — one block per XCD (workgroups go
+  // round-robin over the 8 XCDs, and block 0's XCD need not start first) — recorded at once rather than
+  // held in registers to the end.  (A start atomic from every wave serialised ~6k same-address device atomics ahead
+  // of the first barrier: scene 0 +8 ms, profiles/r04_ab_v17_scene0.jsonl; eight are noise.)
+  if (A.span && blockIdx.x < 8u && threadIdx.x == 0)
+    atomicMax(A.span, static_cast<unsigned long long>(~__builtin_amdgcn_s_memrealtime()));
   Mem<LDS> S{A.scene};
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
@@ -1886,6 +1887,26 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   // 32-bit per-lane offsets
   // the wave's RNG slot in LDS (32-bit words, one per lane and state word)
   uint32_t *const rng_slot = g_lds + A.rng_slot_word + wave * kRngSlotWords;
+  // tiles: tw = 1 << ts pixels wide, 64 / tw = 1 << tsh tall (pixel k of a tile at row k >> ts, column k & (tw - 1))
+  constexpr uint32_t kTs = (static_cast<uint32_t>(F) >> kVarTileShift) & 7u;   // 0: the offline kernels read it
+  const uint32_t ts = kTs ? kTs : A.tile_shift, tsh = 6u - ts, twm = (1u << ts) - 1u;
+  constexpr bool STAGE = (F & kVarStage) != 0;
+  // Output staging (coalesced tile writes to the HBM frame): a whole tile handed to a wave takes the wave's next
+  // staging slot if it is free (else its pixels are stored when they end, as before).  A lane whose pixel ends parks
+  // its floats in the slot (pixel k at 3 k) and sets bit k of the slot's done mask; the lane that sets the last bit
+  // flags the slot, and at the top of the next round — every lane of the wave active — the wave stores the tile:
+  // lane l writes floats l, l + 64, l + 128 of the tile, so each store instruction covers a contiguous run of a tile
+  // row (a 32-pixel row of a 32-aligned frame: three whole 128-B lines), and the PPM bytes of the same floats
+  // (pixels_to_ppm, fused) likewise.  A lane finds its pixel's slot by the tile id in the slot headers, so nothing
+  // but the one-word "slot complete" flag is carried through the traversal.
+  const uint32_t n_stage = (!STAGE || probe || A.out == nullptr) ? 0u : A.stage_slots;   // wave-uniform
+  uint32_t *const stage = g_lds + __builtin_amdgcn_readfirstlane(A.stage_word + wave * A.stage_slots * kStageSlotWords);
+  uint32_t stage_next = 0;                 // wave-uniform: the slot the next whole tile may take
+  uint32_t stage_full = 0;                 // the lane completed slot stage_full - 1 this round (0: none)
+  if (n_stage != 0u) {
+    if (lane < n_stage) stage[lane * kStageSlotWords + kStageTile] = kStageFree;
+    __threadfence_block();
+  }
   bool exhausted = false;
   bool prio_done = false;                  // wave-uniform: the split costliest tiles are all handed out
   uint32_t tiles_taken = 0, rounds = 0;
@@ -1962,6 +1983,41 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       probe_end = false;
     }
+    // ---- staged tiles whose last pixel ended last round are stored (whole lines per store instruction) ----
+    if (n_stage != 0u) {
+      uint64_t fm = __ballot(stage_full != 0u);
+      if (fm != 0) {
+        // the lane id through a volatile asm: the per-lane entry indices below stay inside this rarely run block
+        // instead of being hoisted out of the render loop (registers live across the whole traversal)
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        __threadfence_block();   // the floats parked and the done bits set last round come first
+        while (fm != 0) {
+          const uint32_t q = __builtin_amdgcn_readlane(stage_full, __builtin_ctzll(fm)) - 1u;
+          fm &= ~__ballot(stage_full == q + 1u);
+          uint32_t *const sq = stage + q * kStageSlotWords;
+          const uint32_t tile = __builtin_amdgcn_readfirstlane(sq[kStageTile]);
+          const uint64_t valid = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(sq[kStageValid + 1])) << 32) |
+                                 __builtin_amdgcn_readfirstlane(sq[kStageValid]);
+          const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
+          const uint32_t lr0 = ty << tsh, j0 = tx << ts;
+          const float *sf = reinterpret_cast<const float *>(sq);
+#pragma unroll
+          for (uint32_t i = 0; i < 3; ++i) {
+            const uint32_t e = ln + 64u * i, k = e / 3u, comp = e - 3u * k;
+            if ((valid >> k) & 1ull) {
+              const size_t pix = static_cast<size_t>(lr0 + (k >> ts)) * static_cast<uint32_t>(A.width) + j0 + (k & twm);
+              const float v = sf[e];
+              A.out[3 * pix + comp] = v;
+              if (A.out8) A.out8[3 * pix + comp] = ppm_byte(v);
+            }
+          }
+          __threadfence_block();   // the slot's reads above come before its release
+          if (ln == 0) sq[kStageTile] = kStageFree;
+        }
+        stage_full = 0u;
+      }
+    }
     // ---- lanes without a pixel take the next pixels of the wave's tile ----
     bool need = !busy;
     uint64_t m = __ballot(need);
@@ -2009,17 +2065,33 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           // slot for the lanes that take those pixels
           const uint32_t id = base + lane;
           uint32_t x0 = 0, x1 = 0, x2 = 0, x3 = 0, x4 = 0, tcol = 0;
+          uint32_t tile = id >> 6;
+          bool valid = false;
           if (id < chunk_end) {
-            uint32_t tile = id >> 6;
             const uint32_t kk = id & 63u;
             if (A.tile_order) tile = A.tile_order[tile];
             const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
-            const uint32_t lr = ty * 8 + (kk >> 3), j = tx * 8 + (kk & 7u);
+            const uint32_t lr = (ty << tsh) + (kk >> ts), j = (tx << ts) + (kk & twm);
             if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
-              const uint32_t *pb = A.rng_rows + (lr * 8 + (kk & 7u)) * 8;
+              // phase base of (lr, j & (tw - 1)) and the column table of J^(tw (j >> ts)): one table per tile
+              const uint32_t *pb = A.rng_rows + ((lr << ts) + (j & twm)) * 8;
               const uint4 rb = *reinterpret_cast<const uint4 *>(pb);
               x0 = rb.x; x1 = rb.y; x2 = rb.z; x3 = rb.w; x4 = pb[4];
-              tcol = tx;
+              tcol = j >> ts;
+              valid = true;
+            }
+          }
+          // a whole tile takes the wave's next staging slot if that slot is free (else it is stored pixel by pixel)
+          if (n_stage != 0u && size == static_cast<uint32_t>(kChunk)) {
+            uint32_t *const sq = stage + stage_next * kStageSlotWords;
+            const uint64_t vm = __ballot(valid);
+            if (__builtin_amdgcn_readfirstlane(sq[kStageTile]) == kStageFree && vm != 0) {
+              if (lane == 0) {
+                sq[kStageDone] = 0u; sq[kStageDone + 1] = 0u;
+                sq[kStageValid] = static_cast<uint32_t>(vm); sq[kStageValid + 1] = static_cast<uint32_t>(vm >> 32);
+                sq[kStageTile] = __builtin_amdgcn_readfirstlane(tile);
+              }
+              stage_next = stage_next + 1u == n_stage ? 0u : stage_next + 1u;
             }
           }
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(A.rng_nib), 0,
@@ -2053,7 +2125,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           if (A.tile_order) tile = A.tile_order[tile];
         }
         const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
-        const uint32_t lr = ty * 8 + (k >> 3), j = tx * 8 + (k & 7u);
+        const uint32_t lr = (ty << tsh) + (k >> ts), j = (tx << ts) + (k & twm);
         if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
           pxy = (lr << 16) | j;
           if constexpr (kCarryPoint) pp = pixel_point();
@@ -2128,7 +2200,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       // a camera ray (no bounce yet, no paused walk) of a shard with candidate lists: its tile's list
       T.atie = 0u;
       if (A.prim_lists && tracing && depth == 0u && !T.active) {
-        T.atie = (pxy >> 19) * A.tiles_x + ((pxy & 0xffffu) >> 3) + 1u;
+        T.atie = (pxy >> (16u + tsh)) * A.tiles_x + ((pxy & 0xffffu) >> ts) + 1u;
       }
     }
     Trace::template run<LDS, COUNT, UV>(S, A, tracing, __ballot(tracing), lane, stk, T, ray, h, vc);
@@ -2363,17 +2435,36 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         probe_end = true;   // its rounds are added to the tile's cost at the top of the next round
         busy = false;
       } else if (sample == A.spp) {
-        const size_t pix = static_cast<size_t>(pxy >> 16) * static_cast<uint32_t>(A.width) + (pxy & 0xffffu);
-        float *o = A.out + 3 * pix;
         const f3 c = mk(sum.x * A.sample_scale, sum.y * A.sample_scale, sum.z * A.sample_scale);
-        o[0] = c.x;
-        o[1] = c.y;
-        o[2] = c.z;
-        if (A.out8) {   // pixels_to_ppm's bytes of the same floats (:1391-1395, 1419-1431), fused
-          uint8_t *b = A.out8 + 3 * pix;
-          b[0] = ppm_byte(c.x);
-          b[1] = ppm_byte(c.y);
-          b[2] = ppm_byte(c.z);
+        uint32_t *sq = nullptr;   // the staging slot of the pixel's tile, if the wave still holds it
+        const uint32_t plr = pxy >> 16, pj = pxy & 0xffffu;
+        if (n_stage != 0u) {
+          const uint32_t ptile = (plr >> tsh) * A.tiles_x + (pj >> ts);
+          for (uint32_t q = 0; q < n_stage; ++q)
+            if (stage[q * kStageSlotWords + kStageTile] == ptile) sq = stage + q * kStageSlotWords;
+        }
+        if (sq != nullptr) {   // parked in the tile's staging slot, stored with the whole tile
+          const uint32_t k = ((plr & ((1u << tsh) - 1u)) << ts) | (pj & twm);
+          float *const d = reinterpret_cast<float *>(sq) + 3u * k;
+          d[0] = c.x;
+          d[1] = c.y;
+          d[2] = c.z;
+          const uint64_t all = (static_cast<uint64_t>(sq[kStageValid + 1]) << 32) | sq[kStageValid];
+          const uint64_t was = atomicOr(reinterpret_cast<unsigned long long *>(sq + kStageDone), 1ull << k);
+          if (((was | (1ull << k)) & all) == all)   // the tile's last pixel: the wave stores it next round
+            stage_full = static_cast<uint32_t>((sq - stage) / kStageSlotWords) + 1u;
+        } else {
+          const size_t pix = static_cast<size_t>(plr) * static_cast<uint32_t>(A.width) + pj;
+          float *o = A.out + 3 * pix;
+          o[0] = c.x;
+          o[1] = c.y;
+          o[2] = c.z;
+          if (A.out8) {   // pixels_to_ppm's bytes of the same floats (:1391-1395, 1419-1431), fused
+            uint8_t *b = A.out8 + 3 * pix;
+            b[0] = ppm_byte(c.x);
+            b[1] = ppm_byte(c.y);
+            b[2] = ppm_byte(c.z);
+          }
         }
         busy = false;
       } else {

@@ -158,9 +158,13 @@ constexpr int kVarByte = 1 << 19;
 // run-time compiled kernels whose colour stack lives in LDS entirely (rc_lds_levels >= max_bounces at any
 // residency, rt_capi.cpp): no HBM level code (the deep unwind's batch registers) in the kernel
 constexpr int kVarRcLds = 1 << 20;
+// run-time compiled kernels with the output staging code (RenderArgs::stage_*; used when the launch gets slots), and
+// the tile shape as a constant (bits 22..24 = RenderArgs::tile_shift; 0: read from RenderArgs, the offline kernels)
+constexpr int kVarStage = 1 << 21;
+constexpr int kVarTileShift = 22;
 // variant bits the run-time compiled kernels are specialised on
 constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop | kVarByte | kVarRcLds |
-                            (15 << kVarMatShift) | (15 << kVarTexShift);
+                            kVarStage | (7 << kVarTileShift) | (15 << kVarMatShift) | (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
@@ -193,14 +197,21 @@ struct RenderArgs {
   float sample_scale;
   uint32_t n_pixels;          // row_count * width (local pixels of this shard)
   uint32_t rows;              // row_count
-  uint32_t tiles_x;           // ceil(width / 8)
-  uint32_t n_ids;             // 64 * ceil(rows/8) * tiles_x: tile-major pixel ids handed to waves
+  uint32_t tiles_x;           // ceil(width / tile width)
+  uint32_t n_ids;             // 64 * ceil(rows / tile height) * tiles_x: tile-major pixel ids handed to waves
+  // Tiles of 64 pixels, tw = 1 << tile_shift wide and 64 / tw tall (3: 8x8, 5: 32x2).  A 32-pixel tile row of the
+  // float frame is 384 B = three whole 128-B lines (W % 32 == 0), so every frame line is written by one wave
+  uint32_t tile_shift;
+  // Output staging (coalesced tile writes): a finished pixel's floats wait in its wave's LDS slot for the tile and the
+  // wave stores the whole tile at once (whole lines, the PPM bytes next to them) when its last pixel ends.
+  // stage_slots tiles per wave (0: every pixel written when it ends), kStageSlotWords each, from LDS word stage_word
+  uint32_t stage_word, stage_slots;
   // RNG seeding fused into the tile pickup (init_gpu_data's curand_init, raytracing.cu:1591-1606): when a wave
   // takes a chunk of pixel ids, lane l applies the column table of its pixel's tile column (rng_nib) to the phase
   // base of its pixel (rng_rows) and leaves the state in the wave's slot; the lanes that take those pixels read
   // their states from there (xorwow_jump.h xorwow_phase_bases / xorwow_column_tables)
-  const uint32_t *rng_rows;   // [rows][8 columns][8] phase bases {x0..x4, pad}: pixel (lr, c), c < 8
-  const uint32_t *rng_nib;    // [tiles_x][kRngNibTableWords]: nibble table of J^(8 t) for tile column t
+  const uint32_t *rng_rows;   // [rows][tw columns][8] phase bases {x0..x4, pad}: pixel (lr, c), c < tw (the tile width)
+  const uint32_t *rng_nib;    // [tiles_x][kRngNibTableWords]: nibble table of J^(tw t) for tile column t
   uint32_t rng_d;             // the Weyl word d (the same for every subsequence)
   uint32_t rng_slot_word;     // LDS word of the block's per-wave slots, [wave][5][64]: the states of the chunk of pixel
                               // ids the wave took last (kRngSlotWords per wave)
@@ -262,6 +273,12 @@ struct RenderArgs {
 // and value v, the XOR of the rows of v's bits: words 0..3 as uint4 [c * 16 + v], then word 4 as u32 [c * 16 + v]
 constexpr uint32_t kRngNibTableWords = 40 * 16 * 5;
 constexpr uint32_t kRngSlotWords = 5 * 64;   // per wave
+// output staging slot (RenderArgs::stage_*): 64 pixels x 3 floats in tile order (pixel k at 3 k), then a header:
+// the finished-pixel mask (u64), the tile (kStageFree: unused slot), the valid-pixel mask (u64) — 8-B aligned
+constexpr uint32_t kStageSlotWords = 192 + 6;
+enum : uint32_t { kStageDone = 192, kStageTile = 194, kStageValid = 196 };
+constexpr uint32_t kStageFree = 0xffffffffu;
+constexpr uint32_t kStageSlotsMax = 4;
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)

@@ -109,7 +109,10 @@ constexpr float kFoldRayBound = 1.0e6f;
 constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr size_t kRngSlotBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kRngSlotWords * 4;   // per block, LDS
-constexpr size_t kRcLdsOnlyBlocks = 6;   // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
+constexpr size_t kStageBlockBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kStageSlotWords * 4;   // per slot, block
+constexpr size_t kRcLdsOnlyBlocks = 6;
+constexpr uint32_t kDefaultTileShift = 3;    // 8x8 tiles
+constexpr uint32_t kDefaultStageSlots = 0;   // pixels stored when they end   // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
@@ -178,6 +181,23 @@ float ray_bound(const rt::SceneImage &img, const rt_camera *cam, const rt_params
   b = std::max(b, 3.0f + fuzz);
   return std::isfinite(b) ? b : INFINITY;
 }   // the probe costs 8 paths per 64-pixel tile: <1% of the frame from here
+
+// Frame-write settings of new contexts (and of rt_kernel_source): tile width RT_TILE_W (8, 16, 32, 64) and output
+// staging slots per wave RT_STAGE_SLOTS (0..kStageSlotsMax)
+uint32_t tile_shift_setting() {
+  uint32_t ts = kDefaultTileShift;
+  if (const char *e = std::getenv("RT_TILE_W")) {
+    const int v = std::atoi(e);
+    ts = v == 8 ? 3u : v == 16 ? 4u : v == 32 ? 5u : v == 64 ? 6u : ts;
+  }
+  return ts;
+}
+uint32_t stage_slots_setting() {
+  uint32_t n = kDefaultStageSlots;
+  if (const char *e = std::getenv("RT_STAGE_SLOTS"))
+    n = static_cast<uint32_t>(std::max(0, std::min(static_cast<int>(rt::kStageSlotsMax), std::atoi(e))));
+  return n;
+}
 
 struct rt_context {
   int device = 0;
@@ -265,6 +285,11 @@ struct rt_context {
   uint32_t rc_audit_code = 4;     // ... holding codes of this many bytes
   bool rc_no_byte = false;        // RT_RC_BYTE=0: 16-bit codes where 8-bit ones would do (A/B)
   bool rc_lds_only_off = false;   // set while a render is redone without kVarRcLds (its layout did not fit)
+  // frame writes (RenderArgs::tile_shift / stage_*): tile width 1 << tile_shift (RT_TILE_W) and the staging slots per
+  // wave (RT_STAGE_SLOTS, 0 = every pixel stored when it ends); the slots only take LDS the resident blocks leave
+  uint32_t tile_shift = 3;         // (tile_shift_setting)
+  uint32_t stage_slots = 0;        // (stage_slots_setting)
+  uint32_t used_stage_slots = 0;   // the last render's
   uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
   double jit_ms = 0.0;            // ... and the host time spent obtaining them
@@ -325,7 +350,8 @@ static double half_motion_of(const std::vector<uint32_t> &prims) {
   return 0.5 * m * (1.0 + 1.0e-9);
 }
 
-static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p, uint32_t tiles_x, double half_motion, float *rho_f);
+static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p, uint32_t tiles_x, uint32_t tile_shift,
+                                       double half_motion, float *rho_f);
 
 int rt_accel_build_quant(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]) {
   if (!scene || !info) return RT_ERR_INVALID_ARG;
@@ -360,7 +386,7 @@ int rt_prim_lists(const rt_scene *scene, const rt_camera *cam, const rt_params *
   const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
   const uint32_t n_tiles = tiles_x * ((static_cast<uint32_t>(p->row_count) + 7) / 8);
   float rf = 0.0f;
-  const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, motion, &rf);
+  const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, 3u, motion, &rf);   // 8x8 tiles (this host API's contract)
   if (rho) *rho = rf;
   std::vector<uint2> buf(cap);
   for (uint32_t t = 0; t < n_tiles; ++t) {
@@ -460,6 +486,8 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_DEFER_LANES")) c->defer_lanes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
   if (const char *e = std::getenv("RT_MIX_PROVE")) c->mix_no_proof = e[0] == '0';
   if (const char *e = std::getenv("RT_RC_BYTE")) c->rc_no_byte = e[0] == '0';
+  c->tile_shift = tile_shift_setting();
+  c->stage_slots = stage_slots_setting();
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     c->accel_lds_set = true;
@@ -538,7 +566,8 @@ int rt_context_render(rt_context *c, const rt_camera *cam, const rt_params *p, f
 // The ray cone geometry of a frame's camera for the primary-ray candidate lists (device/prim_lists.h): the defocus
 // disc's radius bound and the footprint widening cover the float arithmetic of the kernel's camera ray (a few
 // roundings of these magnitudes, far inside 2^-18 of them); *rho_f = the radius bound as a float, rounded up.
-static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p, uint32_t tiles_x, double half_motion, float *rho_f) {
+static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p, uint32_t tiles_x, uint32_t tile_shift,
+                                       double half_motion, float *rho_f) {
   rt::PrimListGeom g{};
   const rtr_vec3 *cv[4] = {&cam->pixel00, &cam->delta_u, &cam->delta_v, &cam->center};
   double *gd[4] = {g.p00, g.du, g.dv, g.c};
@@ -553,6 +582,7 @@ static rt::PrimListGeom make_prim_geom(const rt_camera *cam, const rt_params *p,
   g.eps = 0x1p-18 * (n1(cam->pixel00) + rows_span * n1(cam->delta_v) + (p->width + 1.0) * n1(cam->delta_u) + l1 + g.rho);
   g.width = p->width; g.rows = p->row_count; g.row_offset = p->row_offset; g.row_stride = p->row_stride;
   g.tiles_x = tiles_x;
+  g.tile_shift = tile_shift;
   g.half_motion = half_motion;
   float fr = static_cast<float>(g.rho);
   if (static_cast<double>(fr) < g.rho) fr = std::nextafter(fr, std::numeric_limits<float>::infinity());
@@ -660,7 +690,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
-                        (narrow_ok ? rt::kVarNarrow : 0) | (byte_ok ? rt::kVarByte : 0) | (rc_lds_only ? rt::kVarRcLds : 0);
+                        (narrow_ok ? rt::kVarNarrow : 0) | (byte_ok ? rt::kVarByte : 0) | (rc_lds_only ? rt::kVarRcLds : 0) |
+                        static_cast<int>(c->tile_shift << rt::kVarTileShift) | (c->stage_slots ? rt::kVarStage : 0);
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
   const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
   if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;
@@ -818,6 +849,19 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     if (c->blocks_per_cu > 0) per_cu_lds = std::min(c->blocks_per_cu, per_cu_lds);
     per_cu = std::min(per_cu, per_cu_lds);
   }
+  // output staging slots (coalesced tile writes): as many as the requested number that keep this residency, from the
+  // LDS the blocks leave unused (kLdsReserve per block kept, as above)
+  uint32_t stage_slots = 0;
+  for (uint32_t r = jit_fn ? c->stage_slots : 0u; r > 0 && p->row_count > 0; --r) {   // (kVarStage: run-time kernels)
+    const size_t l = c->lds_bytes + r * kStageBlockBytes;
+    if (static_cast<size_t>(std::max(per_cu, 1)) * (l + kLdsReserve) <= kLdsPerCu) {
+      stage_slots = r;
+      break;
+    }
+  }
+  const size_t stage_base = c->lds_bytes;
+  c->lds_bytes += stage_slots * kStageBlockBytes;
+  c->used_stage_slots = stage_slots;
   const uint32_t rc_lds_words = static_cast<uint32_t>(rc_levels * level_bytes / 4);
   uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
                     static_cast<uint64_t>(c->cu_count);
@@ -825,11 +869,17 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   blocks = std::max<uint64_t>(1, std::min(blocks, needed));
   const uint32_t threads = static_cast<uint32_t>(blocks * rt::kBlock);
   if (std::getenv("RT_DEBUG"))
-    std::fprintf(stderr, "[rt] launch: traversal %d, %d blocks/CU, %llu blocks, lds %zu B (scene %u words, colour-stack levels %u, stack cap %u)\n",
-                 trav, per_cu, static_cast<unsigned long long>(blocks), c->lds_bytes, scene_lds_words, rc_levels, stack_cap);
+    std::fprintf(stderr, "[rt] launch: traversal %d, %d blocks/CU, %llu blocks, lds %zu B (scene %u words, colour-stack levels %u, "
+                 "stack cap %u, tiles %ux%u, staging slots %u)\n",
+                 trav, per_cu, static_cast<unsigned long long>(blocks), c->lds_bytes, scene_lds_words, rc_levels, stack_cap,
+                 1u << c->tile_shift, 64u >> c->tile_shift, stage_slots);
 
-  const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + 7) / 8;
-  const uint32_t n_ids = 64u * ((static_cast<uint32_t>(p->row_count) + 7) / 8) * tiles_x;
+  // tiles of 64 pixels (RenderArgs::tile_shift): 32x2 by default, so that every 128-B line of a 32-aligned float
+  // frame row belongs to one tile (RT_TILE_W = 8 / 16 / 32 / 64)
+  const uint32_t tile_shift = c->tile_shift;
+  const uint32_t tw = 1u << tile_shift, th = 64u >> tile_shift;
+  const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + tw - 1) / tw;
+  const uint32_t n_ids = 64u * ((static_cast<uint32_t>(p->row_count) + th - 1) / th) * tiles_x;
   // RNG: the phase bases of this shard's rows and the column tables (host, once per geometry: a few ms; the
   // per-pixel jumps — one nibble-table product each — run in the render kernel at tile pickup) and the per-wave
   // slots
@@ -838,9 +888,12 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // alternating streams on one context — its render-end event), so a frame still in flight keeps reading the
   // table it was launched with (a blocking null-stream copy did not wait for non-blocking streams).
   {
-    const uint64_t key[5] = {p->seed, static_cast<uint64_t>(p->width), static_cast<uint64_t>(p->row_offset),
-                             static_cast<uint64_t>(p->row_stride), static_cast<uint64_t>(p->row_count)};
-    const bool rows_new = std::memcmp(key, c->rows_key, sizeof key) != 0, cols_new = c->cols_width != p->width;
+    // (phase width = the tile width: every lane of a tile applies the same column table)
+    const uint64_t key[5] = {p->seed, static_cast<uint64_t>(p->width) | (static_cast<uint64_t>(tile_shift) << 32),
+                             static_cast<uint64_t>(p->row_offset), static_cast<uint64_t>(p->row_stride),
+                             static_cast<uint64_t>(p->row_count)};
+    const int cols_key = p->width | static_cast<int>(tile_shift << 24);
+    const bool rows_new = std::memcmp(key, c->rows_key, sizeof key) != 0, cols_new = c->cols_width != cols_key;
     if ((rows_new || cols_new) && c->ev_recorded && hipStreamWaitEvent(s, c->ev[2], 0) != hipSuccess) return RT_ERR_HIP;
     auto upload = [s](DevBuf &dst, PinBuf &stage, const std::vector<uint32_t> &v) {
       const size_t n = v.size() * 4;
@@ -853,15 +906,15 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     };
     if (rows_new) {
       std::vector<uint32_t> rb;
-      rt::xorwow_phase_bases(p->seed, p->width, p->row_offset, p->row_stride, p->row_count, &rb);
+      rt::xorwow_phase_bases(p->seed, p->width, p->row_offset, p->row_stride, p->row_count, &rb, static_cast<int>(tile_shift));
       if (!upload(c->rng_rows, c->rows_stage, rb)) return RT_ERR_HIP;
       std::memcpy(c->rows_key, key, sizeof key);
     }
     if (cols_new) {
       std::vector<uint32_t> ct;
-      rt::xorwow_column_tables(p->width, &ct);
+      rt::xorwow_column_tables(p->width, &ct, static_cast<int>(tile_shift));
       if (!upload(c->rng_cols, c->cols_stage, ct)) return RT_ERR_HIP;
-      c->cols_width = p->width;
+      c->cols_width = cols_key;
     }
   }
   if (c->rc.ensure(static_cast<size_t>(mb) * threads * 4) != hipSuccess) return RT_ERR_HIP;   // (wide codes' size)
@@ -915,6 +968,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.n_pixels = n;
   a.rows = static_cast<uint32_t>(p->row_count);
   a.tiles_x = tiles_x;
+  a.tile_shift = tile_shift;
+  a.stage_slots = stage_slots;
+  a.stage_word = static_cast<uint32_t>(stage_base / 4);   // after the stacks and RNG slots (an even word: 8-B masks)
   a.n_ids = n_ids;
   a.rng_rows = static_cast<const uint32_t *>(c->rng_rows.p);
   a.rng_nib = static_cast<const uint32_t *>(c->rng_cols.p);
@@ -960,7 +1016,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (trav == RT_TRAV_ACCEL && prim_on && c->accel_ok) {
     // primary-ray candidate lists of this frame's camera (device/prim_lists.h), before the probe and the render
     float prim_rho = 0.0f;
-    const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, c->accel_half_motion, &prim_rho);
+    const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, tile_shift, c->accel_half_motion, &prim_rho);
     const uint32_t words = c->accel_half_motion > 0 ? 12u : 8u;
     if (c->prim_lists.ensure(static_cast<size_t>(n_tiles) * c->prim_cap * words * 4) != hipSuccess ||
         c->prim_counts.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
@@ -1242,7 +1298,8 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
                       (img.needs_uv ? rt::kVarUv : 0) | rt::scene_shading_bits(img) |
                       (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0) |
-                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0);
+                      (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0) |
+                      static_cast<int>(tile_shift_setting() << rt::kVarTileShift) | (stage_slots_setting() ? rt::kVarStage : 0);
   {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks)
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
     const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +
@@ -1324,15 +1381,17 @@ int rt_seed_states(uint64_t seed, int width, int row_offset, int row_stride, int
 int rt_rng_table_states(uint64_t seed, int width, int row_offset, int row_stride, int rows, uint32_t *out) {
   if (!out || width <= 0 || rows <= 0 || row_offset < 0 || row_stride <= 0) return RT_ERR_INVALID_ARG;
   std::vector<uint32_t> pb, ct;
-  rt::xorwow_phase_bases(seed, width, row_offset, row_stride, rows, &pb);
-  rt::xorwow_column_tables(width, &ct);
+  const int ph = static_cast<int>(tile_shift_setting());   // the phase width of a new context's renders (the tile width)
+  const int pw = 1 << ph;
+  rt::xorwow_phase_bases(seed, width, row_offset, row_stride, rows, &pb, ph);
+  rt::xorwow_column_tables(width, &ct, ph);
   uint32_t base[6];
   rt::xorwow_seed_base(seed, base);
   for (int lr = 0; lr < rows; ++lr)
-    for (int j = 0; j < width; ++j) {   // the render kernel's pickup: phase base (lr, j & 7), column table j >> 3
+    for (int j = 0; j < width; ++j) {   // the render kernel's pickup: phase base (lr, j & (pw-1)), table j >> ph
       uint32_t x[5];
-      std::memcpy(x, &pb[(static_cast<size_t>(lr) * 8 + (j & 7)) * 8], sizeof x);
-      rt::xorwow_apply_nib(ct.data() + static_cast<size_t>(j >> 3) * rt::kJumpNibbleWords, x);
+      std::memcpy(x, &pb[(static_cast<size_t>(lr) * pw + (j & (pw - 1))) * 8], sizeof x);
+      rt::xorwow_apply_nib(ct.data() + static_cast<size_t>(j >> ph) * rt::kJumpNibbleWords, x);
       uint32_t *o = out + (static_cast<size_t>(lr) * width + j) * 6;
       o[0] = base[0];
       std::memcpy(o + 1, x, sizeof x);

@@ -104,6 +104,16 @@ int rt_multi_row_map(int32_t row_count, int32_t n, int32_t k, int32_t *device, i
   return RT_OK;
 }
 
+int rt_multi_unpermute(const void *gathered_device, void *out_device, int32_t row_count, int32_t n_devices,
+                       int32_t max_rows, uint32_t row_bytes, void *stream) {
+  if (row_count < 0 || n_devices <= 0 || max_rows < 0 || (row_count > 0 && (!gathered_device || !out_device)))
+    return RT_ERR_INVALID_ARG;
+  if (max_rows < shard_rows(row_count, n_devices, 0)) return RT_ERR_INVALID_ARG;
+  return rt::launch_unpermute(gathered_device, out_device, static_cast<uint32_t>(row_count),
+                              static_cast<uint32_t>(n_devices), static_cast<uint32_t>(max_rows), row_bytes,
+                              static_cast<hipStream_t>(stream)) == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
 void rt_multi_destroy(rt_multi *m) {
   if (!m) return;
   const Rccl &R = rccl();

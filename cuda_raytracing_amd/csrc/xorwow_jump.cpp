@@ -118,26 +118,29 @@ void xorwow_row_bases(uint64_t seed, int width, int row_offset, int row_stride, 
   }
 }
 
-void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out) {
+void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out,
+                        int phase) {
+  const int pw = 1 << phase;
   std::vector<uint32_t> rb;
   xorwow_row_bases(seed, width, row_offset, row_stride, rows, &rb);
-  out->assign(static_cast<size_t>(rows > 0 ? rows : 0) * 64, 0u);
+  out->assign(static_cast<size_t>(rows > 0 ? rows : 0) * pw * 8, 0u);
   const std::vector<uint32_t> &T = xorwow_jump_tables();
   for (int lr = 0; lr < rows; ++lr) {
     uint32_t x[5];
     std::memcpy(x, &rb[static_cast<size_t>(lr) * 8], sizeof x);
-    for (int c = 0; c < 8; ++c) {
-      std::memcpy(&(*out)[(static_cast<size_t>(lr) * 8 + c) * 8], x, sizeof x);
+    for (int c = 0; c < pw; ++c) {
+      std::memcpy(&(*out)[(static_cast<size_t>(lr) * pw + c) * 8], x, sizeof x);
       if (c + 1 < width) xorwow_jump_nib(T.data(), 0, x);   // the next column: subsequence + 1 = P_0
     }
   }
 }
 
-void xorwow_column_tables(int width, std::vector<uint32_t> *out) {
-  const int tiles = width > 0 ? (width + 7) / 8 : 0;
+void xorwow_column_tables(int width, std::vector<uint32_t> *out, int phase) {
+  const int pw = 1 << phase;
+  const int tiles = width > 0 ? (width + pw - 1) / pw : 0;
   out->assign(static_cast<size_t>(tiles) * kJumpNibbleWords, 0u);
   const std::vector<uint32_t> &T = xorwow_jump_tables();
-  // M_t = J^(8 t), rows[b] = image of e_b: M_0 = I, M_t = P_3 M_{t-1} (column by column through P_3's table)
+  // M_t = J^(pw t), rows[b] = image of e_b: M_0 = I, M_t = P_phase M_{t-1} (column by column through P_phase's table)
   Mat m;
   for (int b = 0; b < 160; ++b) {
     std::memset(m.r[b], 0, sizeof m.r[b]);
@@ -145,7 +148,7 @@ void xorwow_column_tables(int width, std::vector<uint32_t> *out) {
   }
   for (int t = 0; t < tiles; ++t) {
     if (t > 0)
-      for (int b = 0; b < 160; ++b) xorwow_jump_nib(T.data(), 3, m.r[b]);
+      for (int b = 0; b < 160; ++b) xorwow_jump_nib(T.data(), phase, m.r[b]);
     uint32_t *lo = out->data() + static_cast<size_t>(t) * kJumpNibbleWords;
     uint32_t *hi = lo + kJumpNibbles * 16 * 4;
     for (int c = 0; c < kJumpNibbles; ++c)

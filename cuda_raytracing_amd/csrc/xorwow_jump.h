@@ -26,13 +26,16 @@ void xorwow_jump_nib(const uint32_t *tables, int k, uint32_t x[5]);
 // out[lr * 8 + w] = word x_w (w < 5) of global row row_offset + lr * row_stride, lr < rows.  The Weyl word d is
 // the same for every subsequence (xorwow_seed_base).
 void xorwow_row_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out);
-// The render kernel's seeding tables (one nibble-table jump per pixel at tile pickup):
-//  * phase bases: out[(lr * 8 + c) * 8 + w] = word x_w of the state of pixel (row lr, column c), c < 8 — the row
-//    base jumped over its first 8 columns (columns past the width keep the row base: never read);
-//  * column tables: for tile column t < ceil(width / 8), the nibble table (kJumpNibbleWords, xorwow_jump_nib's
-//    format) of J^(8 t).  Pixel (lr, j) = table[j >> 3] applied to phase base (lr, j & 7): powers of J commute.
-void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out);
-void xorwow_column_tables(int width, std::vector<uint32_t> *out);
+// The render kernel's seeding tables (one nibble-table jump per pixel at tile pickup), for a phase width
+// pw = 1 << phase (the tile width: every lane of a tile then applies the same table):
+//  * phase bases: out[(lr * pw + c) * 8 + w] = word x_w of the state of pixel (row lr, column c), c < pw — the row
+//    base jumped over its first pw columns (columns past the width keep the row base: never read);
+//  * column tables: for column group t < ceil(width / pw), the nibble table (kJumpNibbleWords, xorwow_jump_nib's
+//    format) of J^(pw t).  Pixel (lr, j) = table[j >> phase] applied to phase base (lr, j & (pw - 1)): powers of J
+//    commute.
+void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out,
+                        int phase = 3);
+void xorwow_column_tables(int width, std::vector<uint32_t> *out, int phase = 3);
 // x <- (the matrix of nibble table tab) x
 void xorwow_apply_nib(const uint32_t *tab, uint32_t x[5]);
 

@@ -204,6 +204,12 @@ int rt_render_devices(const rt_scene *scene, const rt_camera *camera, const rt_p
  * *shard_rows = that device's row count, *max_rows = the longest shard (the gather's per-device stride). */
 int rt_multi_row_map(int32_t row_count, int32_t n_devices, int32_t k, int32_t *device, int32_t *local,
                      int32_t *shard_rows, int32_t *max_rows);
+/* The root's un-permute step of rt_multi_render on its own (tests; one device is enough): `gathered` holds n_devices
+ * shards of max_rows rows of row_bytes bytes (device memory; shard g's local row i at (g * max_rows + i) * row_bytes,
+ * rows past a shard's own count are padding and never read), `out` receives row_count rows in frame order (frame row
+ * k = shard k % n_devices, local row k / n_devices), asynchronously on `stream` (NULL: the null stream). */
+int rt_multi_unpermute(const void *gathered_device, void *out_device, int32_t row_count, int32_t n_devices,
+                       int32_t max_rows, uint32_t row_bytes, void *stream);
 
 /* Device tonemap: the byte conversion of pixels_to_ppm (raytracing.cu:1391-1395,
  * 1419-1431) — sqrt gamma, clamp [0, 0.999], (u8)(256 x) — from a device framebuffer of `pixels`

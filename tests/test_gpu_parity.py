@@ -1126,3 +1126,24 @@ def test_seed_tables_stream_ordered_between_queued_frames():
     rc, ref_b, _ = oracle_render(w.scene(), cam_b, pb)
     assert rc == 0 and np.array_equal(bits(out_b.cpu().numpy()), bits(ref_b))
     ctx.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("row_bytes", [111, 444])   # a u8 row of 37 px (not a multiple of 4) and a float row
+def test_multi_unpermute_matches_numpy(n, row_bytes):
+    # the root's un-permute of rt_multi_render (rows dealt round-robin, shards padded to the longest) on one
+    # device: shards shorter than max_rows (their padding rows hold garbage that must never be read), word and byte rows
+    rows = 29
+    max_rows = (rows + n - 1) // n
+    g = np.random.default_rng(row_bytes * 10 + n)
+    gathered = g.integers(0, 256, size=(n, max_rows, row_bytes), dtype=np.uint8)
+    src = torch.from_numpy(gathered).cuda()
+    out = torch.zeros((rows, row_bytes), dtype=torch.uint8, device="cuda")
+    rc = _abi.hip_lib().rt_multi_unpermute(C.c_void_p(src.data_ptr()), C.c_void_p(out.data_ptr()), rows, n, max_rows,
+                                          row_bytes, C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    want = np.stack([gathered[k % n, k // n] for k in range(rows)])
+    assert np.array_equal(out.cpu().numpy(), want)
+    bad = _abi.hip_lib().rt_multi_unpermute(C.c_void_p(src.data_ptr()), C.c_void_p(out.data_ptr()), rows, n,
+                                           max_rows - 1, row_bytes, None)
+    assert bad == _abi.RT_ERR_INVALID_ARG

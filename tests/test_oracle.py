@@ -189,18 +189,20 @@ def test_image_texture_scene_renders():
     assert len(np.unique(fb.reshape(-1, 3), axis=0)) > 50
 
 
+@pytest.mark.parametrize("tile_w", ["8", "32", "64"])
 @pytest.mark.parametrize("width,row_offset,row_stride,rows", [(1920, 0, 1, 3), (37, 3, 5, 17), (3840, 7, 8, 2), (1, 0, 1, 5),
                                                                  (13, 0, 1, 2)])
-def test_rng_table_states_match_the_oracles_seeding(width, row_offset, row_stride, rows):
-    # the render kernel's fused seeding, restated on the host (rt_rng_table_states: phase base of (row, column & 7)
-    # times the column table of J^(8 * (column >> 3)), the tables the kernel reads): every pixel's first draws
-    # equal the oracle's rocrand_init draws for subsequence (global row) * width + column
+def test_rng_table_states_match_the_oracles_seeding(width, row_offset, row_stride, rows, tile_w, monkeypatch):
+    # the render kernel's fused seeding, restated on the host (rt_rng_table_states: phase base of (row, column & (tw-1))
+    # times the column table of J^(tw * (column >> log2 tw)), tw = the tile width, the tables the kernel reads): every
+    # pixel's first draws equal the oracle's rocrand_init draws for subsequence (global row) * width + column
     import ctypes as C
     from cuda_raytracing_amd import _abi
+    monkeypatch.setenv("RT_TILE_W", tile_w)
     st = np.zeros((rows * width, 6), np.uint32)
     assert _abi.hip_lib().rt_rng_table_states(1234, width, row_offset, row_stride, rows, st.ctypes.data_as(C.c_void_p)) == 0
     L = _abi.oracle_lib()
-    cols = sorted(set(range(min(width, 11))) | {width - 1, width // 2, max(0, width - 9)})
+    cols = sorted(set(range(min(width, 11))) | {width - 1, width // 2, max(0, width - 9), min(width - 1, 33), min(width - 1, 70)})
     for k in range(rows):
         for j in cols:
             d, x0, x1, x2, x3, x4 = (int(v) for v in st[k * width + j])
