@@ -480,7 +480,12 @@ struct Trav {
   int sp;          // per-lane hit-stack depth (0 = traversal finished)
   int tc, yc;      // translation / y-rotation cleanup counters
   uint32_t was_last;   // 0/1 in a VGPR (a bool becomes per-join SALU lane-mask merges)
-  bool result;
+  // the walk's hit flag, 0/1 in a VGPR.  It outlives a round in a paused walk (the lane skips shading with `continue`
+  // and resumes next round); held as a bool — a wave-wide lane mask merged with exec at every join — the 4-wide
+  // verified walk built for 6 waves (80 VGPRs, SGPR spills into VGPR lanes) lost it for paused lanes and mis-rendered
+  // random sphere worlds in some pixels, nondeterministically; as a word it is carried like the rest of the
+  // paused state (round-5 diagnosis: DESIGN §2, profiles/r05_w4_diag.txt)
+  uint32_t result;
   // verified traversal paused at the end of a round (resumed next round, shading skipped meanwhile)
   uint32_t active;     // 1 = walk in progress
   uint32_t anode, abest, atie;
@@ -1198,6 +1203,10 @@ struct AccelTraceK {
   // reference record (the fallback walk's hit).
   static constexpr bool kLazyHit = true;
   static constexpr bool kPrimLists = true;   // camera rays may take their tile's candidate list (T.atie)
+  // random_test (drawn before the scatter's rejection, read by a dielectric after it) waits in the lane's traversal
+  // stack (dead from the end of the walk to the next trace) instead of a register: at this kernel's 80-VGPR budget the
+  // allocator otherwise spilled it to scratch once per bounce (scratch stores reach HBM: 10k config)
+  static constexpr bool kParkRandomTest = true;
   template <bool LDS, bool UV>
   __device__ __forceinline__ static void materialize(const Mem<LDS> &S, const RenderArgs &A, const Trav &T, const Ray &r,
                                                      Hit &h) {
@@ -1232,6 +1241,8 @@ template <class TR> __device__ constexpr auto carry_point(int) -> decltype(TR::k
 template <class TR> __device__ constexpr bool carry_point(long) { return false; }
 template <class TR> __device__ constexpr auto prim_lists(int) -> decltype(TR::kPrimLists, bool()) { return TR::kPrimLists; }
 template <class TR> __device__ constexpr bool prim_lists(long) { return false; }
+template <class TR> __device__ constexpr auto park_random_test(int) -> decltype(TR::kParkRandomTest, bool()) { return TR::kParkRandomTest; }
+template <class TR> __device__ constexpr bool park_random_test(long) { return false; }
 
 // ---------------------------------------------------------------------------------------------
 // traversal policy 5: verified traversal of mixed worlds (mixed_accel.cpp)
@@ -1921,6 +1932,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 
   uint32_t pending = 0;   // 1: the lane's rejection sampling continues next round (A.max_tries)
   float random_test = 0.0f;
+  constexpr bool kParkRt = park_random_test<Trace>(0);   // random_test parked in the lane's LDS stack
   const uint32_t try_cap = A.max_tries ? A.max_tries : 0xffffffffu;
   // the pixel's viewport point (:1565-1567), recomputed per sample from pxy (a few ops and no division; three
   // fewer registers carried across the trace)
@@ -2096,7 +2108,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           }
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(A.rng_nib), 0,
                                                                               0x7fffffff, 0x00020000);
-          rng_jump_nib(rs, tcol * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
+          // two table products (J^(tw (t & 15)), then J^(16 tw (t >> 4))): 16 + W / (16 tw) tables in all, so each
+          // XCD's L2 fetches a few hundred KB of them instead of every column group's table
+          rng_jump_nib(rs, (tcol & (kRngColLo - 1u)) * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
+          rng_jump_nib(rs, (kRngColLo + (tcol >> kRngColLoBits)) * kRngNibTableWords * 4u, x0, x1, x2, x3, x4);
           // slot entry id & 63: a chunk is size-aligned (whole tiles, or prio_chunk pieces, a power of two <= 64),
           // so its ids take distinct entries and no chunk base is kept across rounds
           const uint32_t so = id & 63u;
@@ -2231,7 +2246,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       // traversal), so one unlucky lane no longer holds the whole wave in this loop.
       if (!pending) {
         if (COUNT) c_shade++;
-        random_test = rng.uniform();
+        const float rtv = rng.uniform();
+        if constexpr (kParkRt) {   // two u16 stack entries of the lane (the clobber: reloaded, not kept in registers)
+          stk[0] = static_cast<uint16_t>(__float_as_uint(rtv));
+          stk[64] = static_cast<uint16_t>(__float_as_uint(rtv) >> 16);
+          asm volatile("" ::: "memory");
+        } else {
+          random_test = rtv;
+        }
       }
       // Wave-uniform loop: one try per iteration for every lane still rejecting.  It ends when no
       // lane needs a try, after try_cap tries, or once at most A.defer_lanes lanes are left (those
@@ -2340,7 +2362,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         if (!reflect_it) {
           float r0 = (1.0f - ri) / (1.0f + ri);
           r0 = r0 * r0;
-          reflect_it = (r0 + (1.0f - r0) * rt_pow5f(1.0f - cos_t)) > random_test;
+          float rtest = random_test;
+          if constexpr (kParkRt) rtest = __uint_as_float(static_cast<uint32_t>(stk[0]) | (static_cast<uint32_t>(stk[64]) << 16));
+          reflect_it = (r0 + (1.0f - r0) * rt_pow5f(1.0f - cos_t)) > rtest;
         }
         if (reflect_it) {
           dir = sub(ud, scale(2.0f * dot(ud, hn), hn));

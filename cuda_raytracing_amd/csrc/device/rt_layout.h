@@ -211,7 +211,7 @@ struct RenderArgs {
   // base of its pixel (rng_rows) and leaves the state in the wave's slot; the lanes that take those pixels read
   // their states from there (xorwow_jump.h xorwow_phase_bases / xorwow_column_tables)
   const uint32_t *rng_rows;   // [rows][tw columns][8] phase bases {x0..x4, pad}: pixel (lr, c), c < tw (the tile width)
-  const uint32_t *rng_nib;    // [tiles_x][kRngNibTableWords]: nibble table of J^(tw t) for tile column t
+  const uint32_t *rng_nib;    // [kRngColLo + ceil(tiles_x / kRngColLo)][kRngNibTableWords]: J^(tw b), J^(16 tw a)
   uint32_t rng_d;             // the Weyl word d (the same for every subsequence)
   uint32_t rng_slot_word;     // LDS word of the block's per-wave slots, [wave][5][64]: the states of the chunk of pixel
                               // ids the wave took last (kRngSlotWords per wave)
@@ -272,6 +272,9 @@ struct RenderArgs {
 // nibble table of a 160x160 GF(2) jump matrix (xorwow_jump.h): for input nibble c (bits 4c..4c+3 of the state)
 // and value v, the XOR of the rows of v's bits: words 0..3 as uint4 [c * 16 + v], then word 4 as u32 [c * 16 + v]
 constexpr uint32_t kRngNibTableWords = 40 * 16 * 5;
+// column tables in two levels (xorwow_jump.h xorwow_column_tables): J^(tw b) at table b < kRngColLo, J^(kRngColLo tw a)
+// at table kRngColLo + a, for tile column t = kRngColLo a + b
+constexpr uint32_t kRngColLoBits = 4, kRngColLo = 1u << kRngColLoBits;
 constexpr uint32_t kRngSlotWords = 5 * 64;   // per wave
 // output staging slot (RenderArgs::stage_*): 64 pixels x 3 floats in tile order (pixel k at 3 k), then a header:
 // the finished-pixel mask (u64), the tile (kStageFree: unused slot), the valid-pixel mask (u64) — 8-B aligned

@@ -102,6 +102,10 @@ static_assert(rt::CNT_BOUNCES == RT_CNT_BOUNCES && rt::CNT_SHADES == RT_CNT_SHAD
               rt::CNT_OVERFLOW == RT_CNT_STACK_OVERFLOW && rt::CNT_SLOTS == RT_CNT__COUNT, "counter slots");
 static_assert(rt::K_SPHERE == RTR_OBJ_SPHERE && rt::K_BVH == RTR_OBJ_BVH && rt::K_GROUP == RTR_OBJ_GROUP, "kinds");
 
+static_assert(rt::kRngColLo == static_cast<uint32_t>(rt::kColLo) && rt::kRngColLoBits == static_cast<uint32_t>(rt::kColLoBits),
+              "two-level column tables: device and host split");
+static_assert(rt::kRngNibTableWords == static_cast<uint32_t>(rt::kJumpNibbleWords), "nibble table size");
+
 constexpr int kLptMinSpp = 16;
 constexpr uint32_t kAccelMinSpheres = 64;   // smaller all-sphere worlds: the scene-specialised walk
 constexpr uint32_t kPrimMinSpheres = 2048;  // primary-ray candidate lists by default from this many spheres
@@ -192,10 +196,10 @@ uint32_t tile_shift_setting() {
   }
   return ts;
 }
-uint32_t stage_slots_setting() {
-  uint32_t n = kDefaultStageSlots;
-  if (const char *e = std::getenv("RT_STAGE_SLOTS"))
-    n = static_cast<uint32_t>(std::max(0, std::min(static_cast<int>(rt::kStageSlotsMax), std::atoi(e))));
+// (RT_STAGE_SLOTS=-1, A/B only: the staging code compiled in, no slots at launch)
+int stage_slots_setting() {
+  int n = static_cast<int>(kDefaultStageSlots);
+  if (const char *e = std::getenv("RT_STAGE_SLOTS")) n = std::max(-1, std::min(static_cast<int>(rt::kStageSlotsMax), std::atoi(e)));
   return n;
 }
 
@@ -288,7 +292,7 @@ struct rt_context {
   // frame writes (RenderArgs::tile_shift / stage_*): tile width 1 << tile_shift (RT_TILE_W) and the staging slots per
   // wave (RT_STAGE_SLOTS, 0 = every pixel stored when it ends); the slots only take LDS the resident blocks leave
   uint32_t tile_shift = 3;         // (tile_shift_setting)
-  uint32_t stage_slots = 0;        // (stage_slots_setting)
+  int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
   uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
@@ -852,7 +856,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // output staging slots (coalesced tile writes): as many as the requested number that keep this residency, from the
   // LDS the blocks leave unused (kLdsReserve per block kept, as above)
   uint32_t stage_slots = 0;
-  for (uint32_t r = jit_fn ? c->stage_slots : 0u; r > 0 && p->row_count > 0; --r) {   // (kVarStage: run-time kernels)
+  for (uint32_t r = jit_fn ? static_cast<uint32_t>(std::max(c->stage_slots, 0)) : 0u; r > 0 && p->row_count > 0; --r) {
     const size_t l = c->lds_bytes + r * kStageBlockBytes;
     if (static_cast<size_t>(std::max(per_cu, 1)) * (l + kLdsReserve) <= kLdsPerCu) {
       stage_slots = r;
@@ -1391,7 +1395,9 @@ int rt_rng_table_states(uint64_t seed, int width, int row_offset, int row_stride
     for (int j = 0; j < width; ++j) {   // the render kernel's pickup: phase base (lr, j & (pw-1)), table j >> ph
       uint32_t x[5];
       std::memcpy(x, &pb[(static_cast<size_t>(lr) * pw + (j & (pw - 1))) * 8], sizeof x);
-      rt::xorwow_apply_nib(ct.data() + static_cast<size_t>(j >> ph) * rt::kJumpNibbleWords, x);
+      const int t = j >> ph;
+      rt::xorwow_apply_nib(ct.data() + static_cast<size_t>(t & (rt::kColLo - 1)) * rt::kJumpNibbleWords, x);
+      rt::xorwow_apply_nib(ct.data() + static_cast<size_t>(rt::kColLo + (t >> rt::kColLoBits)) * rt::kJumpNibbleWords, x);
       uint32_t *o = out + (static_cast<size_t>(lr) * width + j) * 6;
       o[0] = base[0];
       std::memcpy(o + 1, x, sizeof x);

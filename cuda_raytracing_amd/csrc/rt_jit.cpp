@@ -440,14 +440,14 @@ bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std:
 // The verified sphere walk is latency-bound (dependent node loads): hipRTC allocates its render kernel
 // ~97 VGPRs (4 waves/SIMD); asked for 6 waves (80 VGPRs) it runs the 10k frame 226-231 -> 206-208 ms
 // (profiles/r03_ab_jit_waves.jsonl).  RT_ACCEL_WAVES=N overrides (0: the allocator's own choice);
-// RT_JIT_WAVES, when set, applies to every run-time kernel instead.  The 4-wide walks are asked for 5: their
-// 6-wave build (80 VGPRs, ~23 spilled) mis-rendered two random sphere worlds by an ulp in some pixels while the
-// 5-wave and the allocator's builds matched the oracle (profiles/r04_v14_wide_diag.txt), and 5 is also where the
-// 4-wide walk measured best.
-int accel_waves(int wide) {
+// RT_JIT_WAVES, when set, applies to every run-time kernel instead.  Every width is asked for 6: the round-4
+// mis-render of the 4-wide walk's 6-wave build (a paused walk's hit flag held as a lane-mask bool, lost across the
+// round's `continue` under that register budget; Trav::result is now a word) is gone, 6 waves bit-exact on the
+// random worlds that failed (profiles/r05_w4_diag.txt).
+int accel_waves(int /*wide*/) {
   if (std::getenv("RT_JIT_WAVES")) return 0;
   if (const char *e = std::getenv("RT_ACCEL_WAVES")) return std::max(0, std::min(8, std::atoi(e)));
-  return wide ? 5 : 6;
+  return 6;
 }
 
 // Width of the verified sphere walk's tree: 2 (the SAH BVH2) or 4 (its 4-wide collapse, accel::collapse_wide)

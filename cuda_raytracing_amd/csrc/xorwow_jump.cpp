@@ -137,19 +137,12 @@ void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride
 
 void xorwow_column_tables(int width, std::vector<uint32_t> *out, int phase) {
   const int pw = 1 << phase;
-  const int tiles = width > 0 ? (width + pw - 1) / pw : 0;
-  out->assign(static_cast<size_t>(tiles) * kJumpNibbleWords, 0u);
+  const int groups = width > 0 ? (width + pw - 1) / pw : 0;
+  const int n_hi = (groups + kColLo - 1) / kColLo;
+  out->assign(static_cast<size_t>(kColLo + n_hi) * kJumpNibbleWords, 0u);
   const std::vector<uint32_t> &T = xorwow_jump_tables();
-  // M_t = J^(pw t), rows[b] = image of e_b: M_0 = I, M_t = P_phase M_{t-1} (column by column through P_phase's table)
-  Mat m;
-  for (int b = 0; b < 160; ++b) {
-    std::memset(m.r[b], 0, sizeof m.r[b]);
-    m.r[b][b >> 5] = 1u << (b & 31);
-  }
-  for (int t = 0; t < tiles; ++t) {
-    if (t > 0)
-      for (int b = 0; b < 160; ++b) xorwow_jump_nib(T.data(), phase, m.r[b]);
-    uint32_t *lo = out->data() + static_cast<size_t>(t) * kJumpNibbleWords;
+  auto emit = [&](const Mat &m, int slot) {   // the nibble table of m at table slot `slot`
+    uint32_t *lo = out->data() + static_cast<size_t>(slot) * kJumpNibbleWords;
     uint32_t *hi = lo + kJumpNibbles * 16 * 4;
     for (int c = 0; c < kJumpNibbles; ++c)
       for (int v = 0; v < 16; ++v) {
@@ -160,6 +153,21 @@ void xorwow_column_tables(int width, std::vector<uint32_t> *out, int phase) {
         for (int w = 0; w < 4; ++w) lo[(c * 16 + v) * 4 + w] = r[w];
         hi[c * 16 + v] = r[4];
       }
+  };
+  // low tables J^(pw b), b < kColLo: M_0 = I, M_b = P_phase M_{b-1} (column by column through P_phase's table);
+  // high tables J^(kColLo pw a): M_0 = I, M_a = P_{phase + 4} M_{a-1}
+  for (int level = 0; level < 2; ++level) {
+    Mat m;
+    for (int b = 0; b < 160; ++b) {
+      std::memset(m.r[b], 0, sizeof m.r[b]);
+      m.r[b][b >> 5] = 1u << (b & 31);
+    }
+    const int count = level == 0 ? kColLo : n_hi, k = level == 0 ? phase : phase + kColLoBits;
+    for (int t = 0; t < count; ++t) {
+      if (t > 0)
+        for (int b = 0; b < 160; ++b) xorwow_jump_nib(T.data(), k, m.r[b]);
+      emit(m, level == 0 ? t : kColLo + t);
+    }
   }
 }
 

@@ -30,11 +30,13 @@ void xorwow_row_bases(uint64_t seed, int width, int row_offset, int row_stride, 
 // pw = 1 << phase (the tile width: every lane of a tile then applies the same table):
 //  * phase bases: out[(lr * pw + c) * 8 + w] = word x_w of the state of pixel (row lr, column c), c < pw — the row
 //    base jumped over its first pw columns (columns past the width keep the row base: never read);
-//  * column tables: for column group t < ceil(width / pw), the nibble table (kJumpNibbleWords, xorwow_jump_nib's
-//    format) of J^(pw t).  Pixel (lr, j) = table[j >> phase] applied to phase base (lr, j & (pw - 1)): powers of J
-//    commute.
+//  * column tables, two levels (so that every XCD's L2 holds the few it reads — 46 tables at 3840 px, not 480): for
+//    column group t = j >> phase = kColLo a + b, the nibble tables (kJumpNibbleWords, xorwow_jump_nib's format) of
+//    J^(pw b) at slot b < kColLo and of J^(kColLo pw a) at slot kColLo + a.  Pixel (lr, j) = table[kColLo + a] and
+//    table[b] applied to phase base (lr, j & (pw - 1)): powers of J commute.
 void xorwow_phase_bases(uint64_t seed, int width, int row_offset, int row_stride, int rows, std::vector<uint32_t> *out,
                         int phase = 3);
+constexpr int kColLoBits = 4, kColLo = 1 << kColLoBits;
 void xorwow_column_tables(int width, std::vector<uint32_t> *out, int phase = 3);
 // x <- (the matrix of nibble table tab) x
 void xorwow_apply_nib(const uint32_t *tab, uint32_t x[5]);

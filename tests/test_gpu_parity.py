@@ -1034,6 +1034,22 @@ def test_wide_verified_sphere_traversal_matches_oracle(idx, W, H, spp, quant, mo
 def test_wide_random_sphere_worlds_verified_walk(seed, quant, monkeypatch):
     monkeypatch.setenv("RT_ACCEL_WIDTH", "4")
     monkeypatch.setenv("RT_ACCEL_QUANT", quant)
+    _wide_world_vs_oracle(seed)
+
+
+# the round-4 mis-render (a paused walk's hit flag lost by the 6-wave, register-capped build) on every world that showed
+# it on the r04 trees (seeds 0-6: r05 diagnosis, profiles/r05_w4_diag.txt), at the 6 waves every width now asks for and
+# at 5
+@pytest.mark.parametrize("waves", ["6", "5"])
+@pytest.mark.parametrize("seed", [0, 1, 2, 3, 4, 5, 6])
+def test_wide_walk_paused_state_register_budgets(seed, waves, monkeypatch):
+    monkeypatch.setenv("RT_ACCEL_WIDTH", "4")
+    monkeypatch.setenv("RT_ACCEL_QUANT", "0")
+    monkeypatch.setenv("RT_ACCEL_WAVES", waves)
+    _wide_world_vs_oracle(seed)
+
+
+def _wide_world_vs_oracle(seed):
     w, s = _random_sphere_world(seed)
     cam, W, H = rt.camera_from_settings(s, 64, 36)
     p = rt.make_params(s, W, H, spp=4, bounces=12)
