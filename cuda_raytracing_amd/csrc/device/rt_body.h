@@ -1911,13 +1911,56 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   // (pixels_to_ppm, fused) likewise.  A lane finds its pixel's slot by the tile id in the slot headers, so nothing
   // but the one-word "slot complete" flag is carried through the traversal.
   const uint32_t n_stage = (!STAGE || probe || A.out == nullptr) ? 0u : A.stage_slots;   // wave-uniform
-  uint32_t *const stage = g_lds + __builtin_amdgcn_readfirstlane(A.stage_word + wave * A.stage_slots * kStageSlotWords);
+  uint32_t *const stage = g_lds + __builtin_amdgcn_readfirstlane(A.stage_word + wave * (A.stage_slots * kStageSlotWords + 2u));
   uint32_t stage_next = 0;                 // wave-uniform: the slot the next whole tile may take
-  uint32_t stage_full = 0;                 // the lane completed slot stage_full - 1 this round (0: none)
+  // the wave's "slot complete" bits (bit q: slot q's last pixel ended), an LDS word after the slots: set by the lane that
+  // completes a tile, read once per round (no per-lane register carried through the traversal)
+  uint32_t *const stage_done = stage + A.stage_slots * kStageSlotWords;
   if (n_stage != 0u) {
     if (lane < n_stage) stage[lane * kStageSlotWords + kStageTile] = kStageFree;
+    if (lane == 0) *stage_done = 0u;
     __threadfence_block();
   }
+  // the tiles whose last pixel has ended are stored (whole lines per store instruction); every lane of the wave, at a
+  // tile pickup and once the wave's last pixel has ended (no per-round check: nothing is carried through the traversal)
+  auto stage_store = [&]() {
+    uint32_t fm = __builtin_amdgcn_readfirstlane(*stage_done);
+    if (fm == 0) return;
+    // the lane id through a volatile asm: the per-lane entry indices below stay inside this rarely run block instead
+    // of being hoisted out of the render loop (registers live across the whole traversal)
+    uint32_t ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    __threadfence_block();   // the floats parked and the done bits set before come first
+    if (ln == 0) *stage_done = 0u;
+    while (fm != 0) {
+      const uint32_t q = static_cast<uint32_t>(__builtin_ctz(fm));
+      fm &= fm - 1u;
+      uint32_t *const sq = stage + q * kStageSlotWords;
+      const uint32_t tile = __builtin_amdgcn_readfirstlane(sq[kStageTile]);
+      const uint64_t valid = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(sq[kStageValid + 1])) << 32) |
+                             __builtin_amdgcn_readfirstlane(sq[kStageValid]);
+      const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
+      const uint32_t lr0 = ty << tsh, j0 = tx << ts;
+      const float *sf = reinterpret_cast<const float *>(sq);
+#pragma unroll
+      for (uint32_t i = 0; i < 3; ++i) {
+        const uint32_t e = ln + 64u * i, k = e / 3u, comp = e - 3u * k;
+        if ((valid >> k) & 1ull) {
+          const size_t pix = static_cast<size_t>(lr0 + (k >> ts)) * static_cast<uint32_t>(A.width) + j0 + (k & twm);
+          const float v = sf[e];
+          A.out[3 * pix + comp] = v;
+          if (A.out8) A.out8[3 * pix + comp] = ppm_byte(v);
+        }
+      }
+      __threadfence_block();   // the slot's reads above come before its release
+      if (ln == 0) sq[kStageTile] = kStageFree;
+    }
+  };
+  // XCD classes (A.cls_off): the wave's XCD, the queue it draws from (lane 0's count of drained queues) and the rank
+  // in its class of the chunk being handed out
+  const uint32_t xcd = A.cls_off ? (__builtin_amdgcn_s_getreg(20 | (15 << 11)) & (kXcdClasses - 1u)) : 0u;   // HW_REG_XCC_ID
+  uint32_t cls_step = 0;
+  bool chunk_hot = false;
   bool exhausted = false;
   bool prio_done = false;                  // wave-uniform: the split costliest tiles are all handed out
   uint32_t tiles_taken = 0, rounds = 0;
@@ -1995,41 +2038,6 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       }
       probe_end = false;
     }
-    // ---- staged tiles whose last pixel ended last round are stored (whole lines per store instruction) ----
-    if (n_stage != 0u) {
-      uint64_t fm = __ballot(stage_full != 0u);
-      if (fm != 0) {
-        // the lane id through a volatile asm: the per-lane entry indices below stay inside this rarely run block
-        // instead of being hoisted out of the render loop (registers live across the whole traversal)
-        uint32_t ln;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-        __threadfence_block();   // the floats parked and the done bits set last round come first
-        while (fm != 0) {
-          const uint32_t q = __builtin_amdgcn_readlane(stage_full, __builtin_ctzll(fm)) - 1u;
-          fm &= ~__ballot(stage_full == q + 1u);
-          uint32_t *const sq = stage + q * kStageSlotWords;
-          const uint32_t tile = __builtin_amdgcn_readfirstlane(sq[kStageTile]);
-          const uint64_t valid = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(sq[kStageValid + 1])) << 32) |
-                                 __builtin_amdgcn_readfirstlane(sq[kStageValid]);
-          const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
-          const uint32_t lr0 = ty << tsh, j0 = tx << ts;
-          const float *sf = reinterpret_cast<const float *>(sq);
-#pragma unroll
-          for (uint32_t i = 0; i < 3; ++i) {
-            const uint32_t e = ln + 64u * i, k = e / 3u, comp = e - 3u * k;
-            if ((valid >> k) & 1ull) {
-              const size_t pix = static_cast<size_t>(lr0 + (k >> ts)) * static_cast<uint32_t>(A.width) + j0 + (k & twm);
-              const float v = sf[e];
-              A.out[3 * pix + comp] = v;
-              if (A.out8) A.out8[3 * pix + comp] = ppm_byte(v);
-            }
-          }
-          __threadfence_block();   // the slot's reads above come before its release
-          if (ln == 0) sq[kStageTile] = kStageFree;
-        }
-        stage_full = 0u;
-      }
-    }
     // ---- lanes without a pixel take the next pixels of the wave's tile ----
     bool need = !busy;
     uint64_t m = __ballot(need);
@@ -2040,6 +2048,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     uint32_t nhot = sparse ? static_cast<uint32_t>(__popcll(__ballot(busy && hot))) : 0u;
     while (m != 0 && !exhausted) {
       if (chunk_pos >= chunk_end) {
+        if (n_stage != 0u) stage_store();   // the wave's finished tiles first (their slots become free)
         if (sparse && !A.prio_mix && (nhot >= A.prio_lanes || (nhot > 0 && prio_done))) break;
         // the costliest tiles (the first prio_ids ids of the longest-first order) may be handed out in
         // prio_chunk-pixel pieces from their own counter, so that their long pixel chains spread over
@@ -2052,9 +2061,29 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           if (split) base = atomicAdd(A.work + 1, A.prio_chunk);
           if (!split || base >= A.prio_ids) {
             if (sparse && !A.prio_mix && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
-            else base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
+            else if (!A.cls_off)
+              base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
           } else {
             size = A.prio_chunk;
+          }
+        }
+        if (A.cls_off) {
+          // XCD classes (whole tiles only): this wave's XCD queue — tiles whose frame lines no other XCD writes, so the
+          // XCD's L2 merges their partial lines into whole ones — then, once it is drained, the other queues in turn.
+          // Wave-uniform (scalar registers); lane 0 takes the ids
+          for (;;) {
+            const uint32_t q = (xcd + cls_step) & (kXcdClasses - 1u);
+            const uint32_t lo = A.cls_off[q], hi = A.cls_off[q + 1];   // positions in the tile order
+            uint32_t b = 0;
+            if (lane == 0) b = atomicAdd(A.work + kClsWord + q, static_cast<uint32_t>(kChunk));
+            b = __builtin_amdgcn_readfirstlane(b);
+            if (b < (hi - lo) * static_cast<uint32_t>(kChunk)) {
+              base = lo * static_cast<uint32_t>(kChunk) + b;
+              // the chunk is among the costliest if its rank in its class is (each class holds ~1/8 of them)
+              chunk_hot = b < A.prio_ids / kXcdClasses;
+              break;
+            }
+            if (++cls_step == kXcdClasses) { base = A.n_ids; break; }
           }
         }
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
@@ -2146,7 +2175,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           if constexpr (kCarryPoint) pp = pixel_point();
           need = false;
           busy = true;
-          hot = id < A.prio_ids;
+          hot = A.cls_off ? chunk_hot : id < A.prio_ids;
           if (probe) {                      // throwaway stream: the real ones are not consumed
             probe_tile = tile;
             probe_rounds = 0;
@@ -2476,7 +2505,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           const uint64_t all = (static_cast<uint64_t>(sq[kStageValid + 1]) << 32) | sq[kStageValid];
           const uint64_t was = atomicOr(reinterpret_cast<unsigned long long *>(sq + kStageDone), 1ull << k);
           if (((was | (1ull << k)) & all) == all)   // the tile's last pixel: the wave stores it next round
-            stage_full = static_cast<uint32_t>((sq - stage) / kStageSlotWords) + 1u;
+            atomicOr(stage_done, 1u << static_cast<uint32_t>((sq - stage) / kStageSlotWords));
         } else {
           const size_t pix = static_cast<size_t>(plr) * static_cast<uint32_t>(A.width) + pj;
           float *o = A.out + 3 * pix;
@@ -2502,6 +2531,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     }
   }
 
+  if (n_stage != 0u) stage_store();   // every pixel of the wave has ended: the tiles still parked
   if (A.span && lane == 0)   // vector atomics from one lane per wave: first start (above), last end of the launch
     atomicMax(A.span + 1, static_cast<unsigned long long>(__builtin_amdgcn_s_memrealtime()));
   if (TRACE && A.wave_trace && lane == 0) {

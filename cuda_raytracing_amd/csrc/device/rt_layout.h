@@ -204,8 +204,12 @@ struct RenderArgs {
   uint32_t tile_shift;
   // Output staging (coalesced tile writes): a finished pixel's floats wait in its wave's LDS slot for the tile and the
   // wave stores the whole tile at once (whole lines, the PPM bytes next to them) when its last pixel ends.
-  // stage_slots tiles per wave (0: every pixel written when it ends), kStageSlotWords each, from LDS word stage_word
+  // stage_slots tiles per wave (0: every pixel written when it ends), kStageSlotWords each, then the wave's word of
+  // "slot complete" bits and a pad word (per wave stage_slots * kStageSlotWords + 2), from LDS word stage_word
   uint32_t stage_word, stage_slots;
+  // XCD classes (non-null: tile_order is grouped by class, cls_off[q] = class q's first position, cls_off[8] = tiles):
+  // a wave takes its XCD's class first (work[kClsWord + q]: class q's counter), then steals from the others
+  const uint32_t *cls_off;
   // RNG seeding fused into the tile pickup (init_gpu_data's curand_init, raytracing.cu:1591-1606): when a wave
   // takes a chunk of pixel ids, lane l applies the column table of its pixel's tile column (rng_nib) to the phase
   // base of its pixel (rng_rows) and leaves the state in the wave's slot; the lanes that take those pixels read
@@ -282,6 +286,7 @@ constexpr uint32_t kStageSlotWords = 192 + 6;
 enum : uint32_t { kStageDone = 192, kStageTile = 194, kStageValid = 196 };
 constexpr uint32_t kStageFree = 0xffffffffu;
 constexpr uint32_t kStageSlotsMax = 4;
+constexpr uint32_t kXcdClasses = 8, kClsWord = 36;   // (work words 16..35: the mixed walk's RT_MIX_DIAG counters)
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)

@@ -114,6 +114,7 @@ constexpr size_t kLdsPerCu = 160 * 1024;       // gfx950
 constexpr size_t kLdsReserve = 1024;           // per resident block, see the colour-stack sizing
 constexpr size_t kRngSlotBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kRngSlotWords * 4;   // per block, LDS
 constexpr size_t kStageBlockBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kStageSlotWords * 4;   // per slot, block
+constexpr size_t kStageWaveExtraBytes = static_cast<size_t>(rt::kWavesPerBlock) * 2 * 4;   // each wave's flag + pad words
 constexpr size_t kRcLdsOnlyBlocks = 6;
 constexpr uint32_t kDefaultTileShift = 3;    // 8x8 tiles
 constexpr uint32_t kDefaultStageSlots = 0;   // pixels stored when they end   // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
@@ -294,6 +295,9 @@ struct rt_context {
   uint32_t tile_shift = 3;         // (tile_shift_setting)
   int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
+  // per-XCD tile queues (RenderArgs::cls_off; RT_XCD_CLASSES=1/0)
+  bool xcd_classes = false;
+  bool used_classes = false;
   uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
   double jit_ms = 0.0;            // ... and the host time spent obtaining them
@@ -491,6 +495,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_MIX_PROVE")) c->mix_no_proof = e[0] == '0';
   if (const char *e = std::getenv("RT_RC_BYTE")) c->rc_no_byte = e[0] == '0';
   c->tile_shift = tile_shift_setting();
+  if (const char *e = std::getenv("RT_XCD_CLASSES")) c->xcd_classes = e[0] == '1';
   c->stage_slots = stage_slots_setting();
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
@@ -857,14 +862,14 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // LDS the blocks leave unused (kLdsReserve per block kept, as above)
   uint32_t stage_slots = 0;
   for (uint32_t r = jit_fn ? static_cast<uint32_t>(std::max(c->stage_slots, 0)) : 0u; r > 0 && p->row_count > 0; --r) {
-    const size_t l = c->lds_bytes + r * kStageBlockBytes;
+    const size_t l = c->lds_bytes + r * kStageBlockBytes + kStageWaveExtraBytes;
     if (static_cast<size_t>(std::max(per_cu, 1)) * (l + kLdsReserve) <= kLdsPerCu) {
       stage_slots = r;
       break;
     }
   }
   const size_t stage_base = c->lds_bytes;
-  c->lds_bytes += stage_slots * kStageBlockBytes;
+  c->lds_bytes += stage_slots ? stage_slots * kStageBlockBytes + kStageWaveExtraBytes : 0u;
   c->used_stage_slots = stage_slots;
   const uint32_t rc_lds_words = static_cast<uint32_t>(rc_levels * level_bytes / 4);
   uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
@@ -1054,7 +1059,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     // longest-first schedule: probe probe_per_tile throwaway 1-spp paths per tile (their own RNG,
     // no output), then counting-sort tiles by probe cost; counted in render_ms
     if (c->tile_cost.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess ||
-        c->tile_order.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
+        c->tile_order.ensure((static_cast<size_t>(n_tiles) + 16) * 4) != hipSuccess)   // + the class offsets
       return RT_ERR_HIP;
     if (hipMemsetAsync(c->tile_cost.p, 0, static_cast<size_t>(n_tiles) * 4, s) != hipSuccess) return RT_ERR_HIP;
     rt::RenderArgs pa = a;
@@ -1075,9 +1080,17 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                     : rt::launch_render(pa, c->variant & ~rt::kVarCount, static_cast<uint32_t>(blocks),
                                                         c->lds_bytes, s);
     if (pe != hipSuccess) return RT_ERR_HIP;
-    if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), s) != hipSuccess)
+    // XCD classes (RT_XCD_CLASSES): 8x8 tiles handed out whole, no sparse / mixed hot waves — per-XCD queues, so that
+    // each 128-B line of the frame is written through one XCD's L2
+    const bool mix_sched0 = c->prio_mix == 1 || (c->prio_mix < 0 && c->used_traversal == RT_TRAV_MIXED);
+    const bool classes = c->xcd_classes && tile_shift == 3u && !mix_sched0 && !(c->img.has_noise && c->coop_noise) &&
+                         (c->prio_chunk < 0 || c->prio_chunk >= 64) && (c->prio_lanes == 0 || c->prio_lanes >= 64);
+    if (rt::launch_order(pa.probe_cost, n_tiles, static_cast<uint32_t *>(c->tile_order.p), classes ? tiles_x : 0u, s) !=
+        hipSuccess)
       return RT_ERR_HIP;
     a.tile_order = static_cast<const uint32_t *>(c->tile_order.p);
+    a.cls_off = classes ? static_cast<const uint32_t *>(c->tile_order.p) + n_tiles : nullptr;
+    c->used_classes = classes;
     // noise scenes: sparse hot waves (below) by default, over the 16 costliest tiles; the verified mixed
     // walk: mixed hot waves over the costliest quarter of the tiles (below)
     const bool mix_sched = c->prio_mix == 1 || (c->prio_mix < 0 && c->used_traversal == RT_TRAV_MIXED);
@@ -1111,6 +1124,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // Tail issue priority: on for the verified mixed walk (final_scene 800x800 spp 64: 638-649 -> 598-611 ms
   // per frame), within noise elsewhere (scene 0 -1 %, 10k +1 %; profiles/r03_ab_tail_prio.jsonl)
   a.tail_prio = (c->tail_prio == 1 || (c->tail_prio < 0 && c->used_traversal == RT_TRAV_MIXED)) ? 1u : 0u;
+  if (std::getenv("RT_DEBUG") && c->used_lpt) std::fprintf(stderr, "[rt] tile queues: %s\n", a.cls_off ? "8 XCD classes" : "one");
   a.span = reinterpret_cast<unsigned long long *>(static_cast<uint32_t *>(c->work.p) + kSpanWord);   // zeroed above
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)

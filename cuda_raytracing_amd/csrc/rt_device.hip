@@ -113,13 +113,18 @@ __global__ __launch_bounds__(kBlock) void seed_kernel(SeedArgs A) {
   }
 }
 
-// Longest-first tile order from the probe costs: bucket by cost (1024 linear buckets of the max,
-// descending), counting sort in LDS.  One block; ~32k tiles at 1080p.  Order inside a bucket is
-// arbitrary — the schedule never changes what a lane computes.
-constexpr int kOrderThreads = 1024, kOrderBuckets = 1024;
-__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint32_t *cost, uint32_t n, uint32_t *order) {
+// Longest-first tile order from the probe costs: bucket by cost (linear buckets of the max, descending), counting
+// sort in LDS.  One block; ~32k tiles at 1080p.  Order inside a bucket is arbitrary — the schedule never changes what
+// a lane computes.  XCD classes (tiles_x != 0): the tiles are first grouped by class — 8x8 tile (tx, ty) -> class
+// ((tx >> 4) + (ty >> 2)) & 7, i.e. 128-pixel column groups shifted every 32 rows, so every 128-B line of the float
+// frame and of the PPM bytes belongs to tiles of one class — then longest-first within the class (128 buckets each);
+// order[n + q] = the first position of class q, order[n + 8] = n (the render kernel's per-XCD queues).
+constexpr int kOrderThreads = 1024, kOrderBuckets = 1024, kOrderClasses = 8;
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint32_t *cost, uint32_t n, uint32_t *order,
+                                                              uint32_t tiles_x) {
   __shared__ uint32_t hist[kOrderBuckets];
   __shared__ uint32_t wmax[kOrderThreads / 64];
+  __shared__ uint32_t wsum[kOrderThreads / 64];
   const uint32_t t = threadIdx.x;
   uint32_t m = 0;
   for (uint32_t i = t; i < n; i += kOrderThreads) m = max(m, cost[i]);
@@ -129,18 +134,35 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint32_t *co
   __syncthreads();
   uint32_t mx = 1;
   for (int w = 0; w < kOrderThreads / 64; ++w) mx = max(mx, wmax[w]);
-  auto key = [&](uint32_t c) {
-    const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(c) * (kOrderBuckets - 1)) / mx);
-    return static_cast<uint32_t>(kOrderBuckets - 1) - b;
+  const uint32_t per = tiles_x ? kOrderBuckets / kOrderClasses : kOrderBuckets;   // cost buckets per class
+  auto key = [&](uint32_t i) {
+    const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(cost[i]) * (per - 1)) / mx);
+    uint32_t k = per - 1 - b;
+    if (tiles_x) {
+      const uint32_t ty = i / tiles_x, tx = i - ty * tiles_x;
+      k += (((tx >> 4) + (ty >> 2)) & (kOrderClasses - 1)) * per;
+    }
+    return k;
   };
-  for (uint32_t i = t; i < n; i += kOrderThreads) atomicAdd(&hist[key(cost[i])], 1u);
+  for (uint32_t i = t; i < n; i += kOrderThreads) atomicAdd(&hist[key(i)], 1u);
   __syncthreads();
-  if (t == 0) {
-    uint32_t run = 0;
-    for (int b = 0; b < kOrderBuckets; ++b) { const uint32_t c = hist[b]; hist[b] = run; run += c; }
+  // exclusive scan of the 1024 bucket counts (one per thread: wave prefix, then the 16 wave totals)
+  const uint32_t v = hist[t];
+  uint32_t incl = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = static_cast<uint32_t>(__shfl_up(static_cast<int>(incl), off));
+    if ((t & 63u) >= static_cast<uint32_t>(off)) incl += u;
   }
+  if ((t & 63u) == 63u) wsum[t >> 6] = incl;
   __syncthreads();
-  for (uint32_t i = t; i < n; i += kOrderThreads) order[atomicAdd(&hist[key(cost[i])], 1u)] = i;
+  uint32_t before = 0;
+  for (uint32_t w = 0; w < (t >> 6); ++w) before += wsum[w];
+  __syncthreads();
+  hist[t] = before + incl - v;
+  __syncthreads();
+  if (tiles_x && t <= kOrderClasses) order[n + t] = t < kOrderClasses ? hist[t * per] : n;
+  __syncthreads();
+  for (uint32_t i = t; i < n; i += kOrderThreads) order[atomicAdd(&hist[key(i)], 1u)] = i;
 }
 
 // linear -> 8-bit sRGB-ish bytes of pixels_to_ppm (raytracing.cu:1391-1395,1419-1431): sqrt gamma
@@ -284,8 +306,8 @@ hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s) {
-  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, s, cost, n, order);
+hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t tiles_x, hipStream_t s) {
+  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, s, cost, n, order, tiles_x);
   return hipGetLastError();
 }
 

@@ -15,7 +15,9 @@ hipError_t launch_seed(const SeedArgs &a, hipStream_t s);
 // pixels_to_ppm byte conversion of n floats (3 per pixel) on the device
 hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_t s);
 // longest-first order of n tiles from probe costs (single block)
-hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, hipStream_t s);
+// tiles_x != 0: grouped into 8 XCD classes (128-pixel column groups of 8x8 tiles), longest-first within each;
+// order[n .. n + 8] = the classes' first positions and n (order must hold n + 9 words)
+hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t tiles_x, hipStream_t s);
 hipError_t launch_render(const RenderArgs &a, int variant, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 // primary-ray candidate lists of the verified sphere walk, one per 8x8 tile of the shard (device/prim_lists.h)
 // (entries of `words` words with the sphere inline, rt_layout.h kPrimEntry*)
