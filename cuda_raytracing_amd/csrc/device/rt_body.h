@@ -1874,6 +1874,27 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
                         : static_cast<uint32_t>(static_cast<const uint16_t *>(A.rc)[i]));
   };
   const uint64_t lt_mask = (1ull << lane) - 1ull;
+  // Deep-level pool (kVarRcPool): levels [rc_lds_levels, mb) of a path go to one of its wave's LDS chunks when one is
+  // free at the path's first such push (else to HBM, as without the pool); the chunk returns to the wave's free mask
+  // when the path's unwind has read it.  Paths that deep are a few lanes of a wave at a time, so chunks for a fraction of
+  // the lanes keep nearly every deep level out of HBM in far fewer LDS bytes than per-lane levels would take.  The mask
+  // is wave-private (taken at the push, returned by LDS atomics at the unwind, program-ordered within the wave)
+  constexpr bool POOL = !RC_LDS && (F & kVarRcPool) != 0;
+  const uint32_t pool_stride = mb > A.rc_lds_levels ? mb - A.rc_lds_levels : 0u;
+  uint32_t *const pool = g_lds + __builtin_amdgcn_readfirstlane(A.rc_pool_word + wave * (1u + A.rc_pool_chunks * pool_stride));
+  uint32_t pc = kRcNoChunk;   // the lane's chunk for its current path's deep levels
+  if (POOL) {
+    if (lane == 0) pool[0] = A.rc_pool_chunks >= 32u ? 0xffffffffu : (1u << A.rc_pool_chunks) - 1u;
+    __threadfence_block();
+  }
+  auto rc_deep_store = [&](uint32_t k, uint32_t code) {
+    if (POOL && pc != kRcNoChunk) pool[1u + pc * pool_stride + (k - A.rc_lds_levels)] = code;
+    else rc_hbm_store(k, code);
+  };
+  auto rc_deep_load = [&](uint32_t k) -> uint32_t {
+    if (POOL && pc != kRcNoChunk) return pool[1u + pc * pool_stride + (k - A.rc_lds_levels)];
+    return rc_hbm_load(k);
+  };
 
   bool busy = false;                      // lane owns a pixel
   bool hot = false;                       // the pixel is one of the first A.prio_ids handed out
@@ -1937,8 +1958,10 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       fm &= fm - 1u;
       uint32_t *const sq = stage + q * kStageSlotWords;
       const uint32_t tile = __builtin_amdgcn_readfirstlane(sq[kStageTile]);
-      const uint64_t valid = (static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(sq[kStageValid + 1])) << 32) |
-                             __builtin_amdgcn_readfirstlane(sq[kStageValid]);
+      // (readfirstlane returns an int: widened without the cast, the low word's bit 31 would sign-extend into the high
+      // word and mark a partial tile's missing rows valid)
+      const uint64_t valid = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(sq[kStageValid + 1]))) << 32) |
+                             static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(sq[kStageValid]));
       const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
       const uint32_t lr0 = ty << tsh, j0 = tx << ts;
       const float *sf = reinterpret_cast<const float *>(sq);
@@ -2410,8 +2433,36 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         // push the attenuation's code (the emission pushed with it is always 0: only lights emit and
         // lights never scatter, raytracing.cu:439-450 vs :457-488, so the unwind adds +0.0f per level)
         if (push) {
-          if (RC_LDS || rsp < A.rc_lds_levels) rc_lds_store(rsp, code);
-          else rc_hbm_store(rsp, code);
+          if (RC_LDS || rsp < A.rc_lds_levels) {
+            rc_lds_store(rsp, code);
+          } else {
+            if constexpr (POOL) {
+              // the lanes starting their first deep level this round take the lowest free chunks, one each in lane order
+              const bool first = rsp == A.rc_lds_levels;
+              const uint64_t need = __ballot(first);
+              if (need != 0) {
+                const uint32_t fm = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(pool[0]));
+                const uint32_t nfree = static_cast<uint32_t>(__popc(fm));
+                const uint32_t take = min(static_cast<uint32_t>(__popcll(need)), nfree);
+                if (first) {
+                  uint32_t r = static_cast<uint32_t>(__popcll(need & lt_mask));
+                  if (r < nfree) {   // the r-th set bit of fm
+                    uint32_t pos = 0;
+#pragma unroll
+                    for (uint32_t s = 16; s >= 1; s >>= 1) {
+                      const uint32_t c = static_cast<uint32_t>(__popc((fm >> pos) & ((1u << s) - 1u)));
+                      if (r >= c) { r -= c; pos += s; }
+                    }
+                    pc = pos;
+                  }
+                }
+                uint32_t left = fm;
+                for (uint32_t i = 0; i < take; ++i) left &= left - 1u;   // wave-uniform
+                pool[0] = left;   // (every active lane stores the same word)
+              }
+            }
+            rc_deep_store(rsp, code);
+          }
           rsp++;
         }
         depth++;
@@ -2451,7 +2502,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         constexpr int kUnwindBatch = DEEP ? RT_UNWIND_BATCH : 1;
         uint32_t cw[kUnwindBatch];
 #pragma unroll
-        for (int i = 0; i < kUnwindBatch; ++i) cw[i] = rc_hbm_load(static_cast<uint32_t>(max(k - i, kl)));
+        for (int i = 0; i < kUnwindBatch; ++i) cw[i] = rc_deep_load(static_cast<uint32_t>(max(k - i, kl)));
         f3 at[kUnwindBatch];
         rc_decode_batch<LDS, WIDE, NOISE, UV>(S, A, cw, at);
 #pragma unroll
@@ -2474,6 +2525,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         for (int i = 0; i < kLdsBatch; ++i) {
           if (k - i < 0) at[i] = mk(1.0f, 1.0f, 1.0f);
           res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
+        }
+      }
+      if constexpr (POOL) {   // the path's pool chunk (read above, or skipped with a black path) is free again
+        if (pc != kRcNoChunk) {
+          atomicOr(pool, 1u << pc);
+          pc = kRcNoChunk;
         }
       }
       if (TRACE) {   // the unwind's share of the done block (the rest: camera ray / pixel write)

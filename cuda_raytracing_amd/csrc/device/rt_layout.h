@@ -162,9 +162,11 @@ constexpr int kVarRcLds = 1 << 20;
 // the tile shape as a constant (bits 22..24 = RenderArgs::tile_shift; 0: read from RenderArgs, the offline kernels)
 constexpr int kVarStage = 1 << 21;
 constexpr int kVarTileShift = 22;
+// run-time compiled kernels with HBM colour-stack levels and the per-wave deep-level pool (RenderArgs::rc_pool_*)
+constexpr int kVarRcPool = 1 << 25;
 // variant bits the run-time compiled kernels are specialised on
 constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop | kVarByte | kVarRcLds |
-                            kVarStage | (7 << kVarTileShift) | (15 << kVarMatShift) | (15 << kVarTexShift);
+                            kVarStage | (7 << kVarTileShift) | kVarRcPool | (15 << kVarMatShift) | (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling
@@ -188,6 +190,10 @@ struct RenderArgs {
   uint32_t off_mats, off_texs, off_perlin, off_pixels, pixel_words;
   uint32_t root, stack_cap, stack_lds_word;   // per-lane stack region starts at this LDS word
   uint32_t rc_lds_word, rc_lds_levels;        // colour-stack levels [0, rc_lds_levels) live in LDS
+  // Deep-level pool (kVarRcPool kernels): per wave, from LDS word rc_pool_word + wave * (1 + rc_pool_chunks * (max_bounces
+  // - rc_lds_levels)), a free-chunk mask word, then rc_pool_chunks chunks of max_bounces - rc_lds_levels words.  A path's
+  // levels past the LDS ones go to a chunk when one is free at its first such push, else to HBM (rc)
+  uint32_t rc_pool_word, rc_pool_chunks;
   uint32_t rc_tex0, rc_consts;                // colour records: first texture, first constant
   // camera (rt_camera)
   float p00[3], du[3], dv[3], center[3], dfu[3], dfv[3], defocus_angle;
@@ -290,6 +296,8 @@ constexpr uint32_t kXcdClasses = 8, kClsWord = 36;   // (work words 16..35: the 
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)
+constexpr uint32_t kRcPoolChunksMax = 32;   // deep-level pool chunks per wave (one mask word)
+constexpr uint32_t kRcNoChunk = 0xffffffffu;
 
 struct SeedArgs {
   const uint32_t *jump;       // xorwow_jump_tables() on device

@@ -115,9 +115,10 @@ constexpr size_t kLdsReserve = 1024;           // per resident block, see the co
 constexpr size_t kRngSlotBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kRngSlotWords * 4;   // per block, LDS
 constexpr size_t kStageBlockBytes = static_cast<size_t>(rt::kWavesPerBlock) * rt::kStageSlotWords * 4;   // per slot, block
 constexpr size_t kStageWaveExtraBytes = static_cast<size_t>(rt::kWavesPerBlock) * 2 * 4;   // each wave's flag + pad words
-constexpr size_t kRcLdsOnlyBlocks = 6;
+constexpr size_t kRcLdsOnlyBlocks = 6;      // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
 constexpr uint32_t kDefaultTileShift = 3;    // 8x8 tiles
-constexpr uint32_t kDefaultStageSlots = 0;   // pixels stored when they end   // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
+constexpr uint32_t kDefaultStageSlots = 0;   // pixels stored when they end
+constexpr int kDefaultRcPool = 0;            // deep-level pool chunks per wave of deep kernels with HBM levels (RT_RC_POOL)
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
@@ -201,6 +202,17 @@ uint32_t tile_shift_setting() {
 int stage_slots_setting() {
   int n = static_cast<int>(kDefaultStageSlots);
   if (const char *e = std::getenv("RT_STAGE_SLOTS")) n = std::max(-1, std::min(static_cast<int>(rt::kStageSlotsMax), std::atoi(e)));
+  return n;
+}
+// Deep-level pool chunks per wave (RT_RC_POOL, 0..kRcPoolChunksMax; RenderArgs::rc_pool_*).  Default: deep kernels
+// (max_bounces > kDeepBounces) whose colour stack does not fit LDS; set explicitly: every kernel with HBM levels
+int rc_pool_setting(bool *set = nullptr) {
+  int n = kDefaultRcPool;
+  if (set) *set = false;
+  if (const char *e = std::getenv("RT_RC_POOL")) {
+    n = std::max(0, std::min(static_cast<int>(rt::kRcPoolChunksMax), std::atoi(e)));
+    if (set) *set = true;
+  }
   return n;
 }
 
@@ -295,6 +307,9 @@ struct rt_context {
   uint32_t tile_shift = 3;         // (tile_shift_setting)
   int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
+  int rc_pool = 0;                 // deep-level pool chunks per wave (rc_pool_setting)
+  bool rc_pool_set = false;        // ... given explicitly: also for shallow kernels
+  uint32_t used_pool_chunks = 0;   // the last render's
   // per-XCD tile queues (RenderArgs::cls_off; RT_XCD_CLASSES=1/0)
   bool xcd_classes = false;
   bool used_classes = false;
@@ -497,6 +512,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   c->tile_shift = tile_shift_setting();
   if (const char *e = std::getenv("RT_XCD_CLASSES")) c->xcd_classes = e[0] == '1';
   c->stage_slots = stage_slots_setting();
+  c->rc_pool = rc_pool_setting(&c->rc_pool_set);
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     c->accel_lds_set = true;
@@ -696,11 +712,14 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
   const bool rc_lds_only = c->rc_lds_auto && !c->rc_lds_only_off && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
+  // the deep-level pool's code in run-time kernels with HBM levels (sized below, once the residency is known)
+  const bool pool_kernel = c->rc_pool > 0 && !rc_lds_only && (mb > static_cast<uint32_t>(rt::kDeepBounces) || c->rc_pool_set);
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
                         (narrow_ok ? rt::kVarNarrow : 0) | (byte_ok ? rt::kVarByte : 0) | (rc_lds_only ? rt::kVarRcLds : 0) |
-                        static_cast<int>(c->tile_shift << rt::kVarTileShift) | (c->stage_slots ? rt::kVarStage : 0);
+                        static_cast<int>(c->tile_shift << rt::kVarTileShift) | (c->stage_slots ? rt::kVarStage : 0) |
+                        (pool_kernel ? rt::kVarRcPool : 0);
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
   const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
   if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;
@@ -858,6 +877,35 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     if (c->blocks_per_cu > 0) per_cu_lds = std::min(c->blocks_per_cu, per_cu_lds);
     per_cu = std::min(per_cu, per_cu_lds);
   }
+  // Deep-level pool (kVarRcPool kernels): rc_pool chunks per wave of the levels past the LDS ones.  With automatic
+  // levels the pool takes its bytes from the per-lane levels (the most levels that fit beside it at this residency);
+  // with pinned levels (RT_RC_LDS_LEVELS) it is added if the residency keeps it.  Fewer chunks if neither fits.
+  uint32_t pool_chunks = 0;
+  size_t pool_base = c->lds_bytes, pool_bytes = 0;
+  if (jit_fn && pool_kernel) {
+    const size_t fixed = c->lds_bytes - rc_levels * level_bytes;   // scene (or SAH top nodes), stacks, RNG slots
+    const size_t cap = kLdsPerCu / static_cast<size_t>(std::max(per_cu, 1)) - kLdsReserve;
+    auto bytes_of = [&](uint32_t P, uint32_t L) {
+      return static_cast<size_t>(rt::kWavesPerBlock) * (1u + P * (mb > L ? mb - L : 0u)) * 4u;
+    };
+    const uint32_t min_levels = std::max<uint32_t>(c->rc_lds_levels, codes_per_word);
+    uint32_t L = rc_levels;
+    for (uint32_t P = static_cast<uint32_t>(c->rc_pool); P > 0 && rc_levels < mb; --P) {
+      uint32_t l = rc_levels;
+      if (c->rc_lds_auto)
+        while (l > min_levels && fixed + l * level_bytes + bytes_of(P, l) > cap) l -= codes_per_word;
+      if (fixed + l * level_bytes + bytes_of(P, l) <= cap) {
+        pool_chunks = P;
+        L = l;
+        break;
+      }
+    }
+    rc_levels = L;
+    pool_base = fixed + rc_levels * level_bytes;
+    pool_bytes = bytes_of(pool_chunks, rc_levels);   // the mask words even without chunks (the kernel sets them)
+    c->lds_bytes = pool_base + pool_bytes;
+  }
+  c->used_pool_chunks = pool_chunks;
   // output staging slots (coalesced tile writes): as many as the requested number that keep this residency, from the
   // LDS the blocks leave unused (kLdsReserve per block kept, as above)
   uint32_t stage_slots = 0;
@@ -879,9 +927,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const uint32_t threads = static_cast<uint32_t>(blocks * rt::kBlock);
   if (std::getenv("RT_DEBUG"))
     std::fprintf(stderr, "[rt] launch: traversal %d, %d blocks/CU, %llu blocks, lds %zu B (scene %u words, colour-stack levels %u, "
-                 "stack cap %u, tiles %ux%u, staging slots %u)\n",
+                 "stack cap %u, tiles %ux%u, staging slots %u, pool chunks %u)\n",
                  trav, per_cu, static_cast<unsigned long long>(blocks), c->lds_bytes, scene_lds_words, rc_levels, stack_cap,
-                 1u << c->tile_shift, 64u >> c->tile_shift, stage_slots);
+                 1u << c->tile_shift, 64u >> c->tile_shift, stage_slots, pool_chunks);
 
   // tiles of 64 pixels (RenderArgs::tile_shift): 32x2 by default, so that every 128-B line of a 32-aligned float
   // frame row belongs to one tile (RT_TILE_W = 8 / 16 / 32 / 64)
@@ -962,6 +1010,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.mix_no_proof = c->mix_no_proof ? 1u : 0u;
   a.rc_lds_word = scene_lds_words;
   a.rc_lds_levels = rc_levels;
+  a.rc_pool_word = static_cast<uint32_t>(pool_base / 4);
+  a.rc_pool_chunks = pool_chunks;
   a.rc_tex0 = c->img.mat_count;
   a.rc_consts = c->img.rec_consts;
   a.stack_lds_word = scene_lds_words + rc_lds_words;
@@ -1155,6 +1205,7 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->mix_macros = c->mixed_ok ? static_cast<int32_t>(c->mixed.macros) : 0;
   if (!c->rendered) return RT_OK;
   st->rc_lds_levels = static_cast<int32_t>(c->used_rc_levels);
+  st->rc_pool_chunks = static_cast<int32_t>(c->used_pool_chunks);
   st->jit_source = c->jit_source;
   st->jit_ms = c->jit_ms;
   DeviceGuard g(c->device);
@@ -1318,11 +1369,14 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0) |
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0) |
                       static_cast<int>(tile_shift_setting() << rt::kVarTileShift) | (stage_slots_setting() ? rt::kVarStage : 0);
-  {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks)
+  {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks), else the pool's code
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
     const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +
                         (img.words.size() <= rt::kLdsSceneMaxWords ? img.words.size() * 4 : 4096u) + kRngSlotBytes + kLdsReserve;
+    bool pool_set = false;
+    const int pool = rc_pool_setting(&pool_set);
     if (traversal == RT_TRAV_STATIC && need <= kLdsPerCu / kRcLdsOnlyBlocks) variant |= rt::kVarRcLds;
+    else if (pool > 0 && (mb > static_cast<uint32_t>(rt::kDeepBounces) || pool_set)) variant |= rt::kVarRcPool;
   }
   std::string src;
   if (traversal == RT_TRAV_STATIC) {

@@ -144,7 +144,8 @@ typedef struct rt_stats {
                               is the stream-event window around the launch (>= this) */
   double gather_ms;        /* rt_multi_render / rt_render_devices: RCCL gather of the shards + on-device un-permute */
   int32_t devices;         /* devices that rendered the frame (1 for the single-device entry points) */
-  int32_t pad2_;
+  int32_t rc_pool_chunks;  /* deep colour-stack levels: LDS pool chunks per wave of the last render (0: levels past
+                              rc_lds_levels in HBM only; RT_RC_POOL) */
 } rt_stats;
 
 /* rt_stats.jit_source */

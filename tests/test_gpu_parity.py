@@ -752,6 +752,74 @@ def test_colour_stack_hbm_levels_random_worlds(seed, levels, monkeypatch):
     _spill_check(w, s, 48, 27, 8, 50, SPILL_FORCES, {L, L + 1, (L + 3) // 4 * 4})
 
 
+def _pool_render(w, s, W, H, spp, b, force, pool, monkeypatch):
+    monkeypatch.setenv("RT_RC_POOL", str(pool))
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=b)
+    p.flags = force | rt.RT_FLAG_RC_AUDIT
+    return gpu(w.scene(), cam, p), cam, p
+
+
+# ---- deep-level pool (kVarRcPool, RT_RC_POOL): a path's levels past the LDS ones in one of its wave's LDS chunks
+# when one is free at its first deep push, else in HBM.  Few chunks (2: most deep paths overflow to HBM, chunks are
+# taken and returned every round) and many (32), on the static, per-lane and verified sphere walks, bit-exact; the
+# chunks keep levels out of HBM (fewer audited HBM slots than the same render without a pool) ----
+@pytest.mark.parametrize("idx,W,H,spp,forces", [
+    (1, 40, 40, 4, [0, rt.RT_FLAG_FORCE_LANE]),
+    (17, 48, 27, 4, [0, rt.RT_FLAG_FORCE_LANE]),
+    (20, 48, 27, 2, [rt.RT_FLAG_FORCE_ACCEL]),
+])
+def test_colour_stack_pool_vs_oracle(idx, W, H, spp, forces, monkeypatch):
+    monkeypatch.setenv("RT_RC_LDS_LEVELS", "4")
+    w, s = rt.build_scene(idx)
+    cam, W2, H2 = rt.camera_from_settings(s, W, H)
+    rc, ref, _ = oracle_render(w.scene(), cam, rt.make_params(s, W2, H2, spp=spp, bounces=50))
+    assert rc == 0
+    for force in forces:
+        (fb0, st0), _, _ = _pool_render(w, s, W, H, spp, 50, force, 0, monkeypatch)
+        assert st0.rc_pool_chunks == 0 and st0.rc_hbm_slots > 0, (force, st0.traversal)
+        assert np.array_equal(bits(fb0), bits(ref)), (force, st0.traversal)
+        for pool in (2, 32):
+            (fb, st), _, _ = _pool_render(w, s, W, H, spp, 50, force, pool, monkeypatch)
+            assert np.array_equal(bits(fb), bits(ref)), (force, pool, st.traversal)
+            assert 0 < st.rc_pool_chunks <= pool, (force, pool, st.rc_pool_chunks)
+            assert st.rc_lds_levels == st0.rc_lds_levels
+            # (2 chunks: a lane may write a level to HBM in one path and to a chunk in another, so only "not more")
+            assert (st.rc_hbm_slots < st0.rc_hbm_slots) if pool == 32 else (st.rc_hbm_slots <= st0.rc_hbm_slots), \
+                (force, pool, st.rc_hbm_slots, st0.rc_hbm_slots)
+
+
+@pytest.mark.parametrize("seed", [1, 6])
+def test_colour_stack_pool_random_worlds(seed, monkeypatch):
+    # the closed room of test_colour_stack_hbm_levels_random_worlds: many paths reach depth 50, so chunks run out
+    monkeypatch.setenv("RT_RC_LDS_LEVELS", "4")
+    w, s = _random_world(seed)
+    w.box((-20.0, -20.0, -20.0), (20.0, 20.0, 20.0), w.lambert((0.8, 0.75, 0.7)))
+    cam, W, H = rt.camera_from_settings(s, 48, 27)
+    rc, ref, _ = oracle_render(w.scene(), cam, rt.make_params(s, W, H, spp=8, bounces=50))
+    assert rc == 0
+    for force in SPILL_FORCES:
+        for pool in (1, 4, 32):
+            (fb, st), _, _ = _pool_render(w, s, 48, 27, 8, 50, force, pool, monkeypatch)
+            assert np.array_equal(bits(fb), bits(ref)), (force, pool, st.traversal)
+            assert st.rc_pool_chunks > 0 or force == rt.RT_FLAG_FORCE_PACKET, (force, pool)
+
+
+@pytest.mark.parametrize("idx,W,H,spp", [(17, 64, 36, 8), (0, 64, 36, 4)])
+def test_colour_stack_pool_automatic_levels(idx, W, H, spp, monkeypatch):
+    # levels chosen by the host (no RT_RC_LDS_LEVELS): the pool takes its bytes from the per-lane levels at d50
+    w, s = rt.build_scene(idx)
+    cam, W2, H2 = rt.camera_from_settings(s, W, H)
+    rc, ref, _ = oracle_render(w.scene(), cam, rt.make_params(s, W2, H2, spp=spp, bounces=50))
+    assert rc == 0
+    (fb0, st0), _, _ = _pool_render(w, s, W, H, spp, 50, 0, 0, monkeypatch)
+    (fb, st), _, _ = _pool_render(w, s, W, H, spp, 50, 0, 16, monkeypatch)
+    assert np.array_equal(bits(fb0), bits(ref)) and np.array_equal(bits(fb), bits(ref))
+    if st0.rc_lds_levels < 50:   # a kernel with HBM levels: the pool is used, levels give way to it
+        assert st.rc_pool_chunks > 0 and st.rc_lds_levels <= st0.rc_lds_levels
+        assert st.rc_hbm_slots <= st0.rc_hbm_slots
+
+
 @pytest.mark.parametrize("b", [16, 17])
 @pytest.mark.parametrize("idx", [1, 17])
 def test_deep_unwind_switch_vs_oracle(idx, b, monkeypatch):
@@ -1163,3 +1231,30 @@ def test_multi_unpermute_matches_numpy(n, row_bytes):
     bad = _abi.hip_lib().rt_multi_unpermute(C.c_void_p(src.data_ptr()), C.c_void_p(out.data_ptr()), rows, n,
                                            max_rows - 1, row_bytes, None)
     assert bad == _abi.RT_ERR_INVALID_ARG
+
+
+@pytest.mark.parametrize("tile_w,slots", [("8", "1"), ("8", "4"), ("32", "4"), ("8", "-1")])
+@pytest.mark.parametrize("idx,W,H,spp", [(0, 96, 54, 8), (0, 37, 29, 4), (20, 72, 44, 2)])
+def test_staged_tile_writes_partial_tiles(idx, W, H, spp, tile_w, slots, monkeypatch):
+    # output staging (RT_STAGE_SLOTS) with partial tiles at the frame's edges: the float frame and the PPM bytes laid out
+    # back to back in one allocation, then a guard — a store past either must show (round 5 found the valid mask of a
+    # partial tile sign-extended by readfirstlane, which wrote the missing rows' floats into the bytes after the frame)
+    import torch
+    monkeypatch.setenv("RT_TILE_W", tile_w)
+    monkeypatch.setenv("RT_STAGE_SLOTS", slots)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=16)
+    n = W * H * 3
+    buf = torch.full((n * 4 + n + 4096,), 0xA5, dtype=torch.uint8, device="cuda")
+    ctx = rt.RenderContext(w.scene(), 0)
+    ctx.render_into(cam, p, buf.data_ptr(), torch.cuda.current_stream().cuda_stream, buf.data_ptr() + n * 4)
+    ctx.timing()
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy()
+    fb = host[:n * 4].view(np.float32).reshape(H, W, 3)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+    assert np.array_equal(host[n * 4:n * 5].reshape(H, W, 3), rt.tonemap(ref))
+    assert (host[n * 5:] == 0xA5).all()
+    ctx.close()

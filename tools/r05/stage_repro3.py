@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""r05: where do the bad PPM bytes of the first tile row (scene 0 96x54 spp 8 d16, RT_STAGE_SLOTS) come from?"""
+import sys
+from pathlib import Path
+import numpy as np
+REPO = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(REPO)); sys.path.insert(0, str(REPO / "tests"))
+import torch
+import cuda_raytracing_amd as rt
+from conftest import oracle_render, bits
+w, s = rt.build_scene(0)
+cam, W, H = rt.camera_from_settings(s, 96, 54)
+p = rt.make_params(s, W, H, spp=8, bounces=16)
+rc, ref, _ = oracle_render(w.scene(), cam, p)
+want = rt.tonemap(ref)
+for rep in range(int(__import__("os").environ.get("REPS", "3"))):
+    ctx = rt.RenderContext(w.scene(), 0)
+    out = torch.full((H, W, 3), float("nan"), dtype=torch.float32, device="cuda")
+    out8 = torch.full((H, W, 3), 7, dtype=torch.uint8, device="cuda")
+    ctx.render_into(cam, p, out.data_ptr(), torch.cuda.current_stream().cuda_stream, out8.data_ptr())
+    ctx.timing(); torch.cuda.synchronize()
+    o8 = out8.cpu().numpy()
+    bad = (o8 != want).any(-1)
+    print(f"rep {rep}: bad {int(bad.sum())} rows {sorted(set(np.argwhere(bad)[:, 0].tolist()))}", flush=True)
+    # byte triples of the bad pixels: do they equal the expected bytes of some other pixel (same column offset)?
+    flat = {tuple(v) for v in want.reshape(-1, 3).tolist()}
+    got = [tuple(v) for v in o8[bad].tolist()]
+    print("   bad triples that are some pixel's expected bytes:", sum(g in flat for g in got), "of", len(got), flush=True)
+    print("   row 0 got ", o8[0, :6].tolist(), flush=True)
+    print("   row 0 want", want[0, :6].tolist(), flush=True)
+    # float bits of row 0 as bytes?
+    fb = out.cpu().numpy()
+    print("   row 0 float bytes", fb[0, :2].view(np.uint8).tolist(), flush=True)
+    ctx.close()
