@@ -2084,8 +2084,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           if (split) base = atomicAdd(A.work + 1, A.prio_chunk);
           if (!split || base >= A.prio_ids) {
             if (sparse && !A.prio_mix && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
-            else if (!A.cls_off)
+            else if (!A.cls_off) {
               base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
+              // the last tail_ids ids of the order go out in tail_chunk-pixel pieces from their own counter: a wave
+              // then holds at most tail_chunk - 1 pixels it has not started when the queue drains, instead of up to 63
+              // of a whole tile, so the waves' last pixels start (and the waves end) closer together
+              if (A.tail_ids != 0u && base >= A.n_ids - A.tail_ids) {
+                base = A.n_ids - A.tail_ids + atomicAdd(A.work + kTailWord, A.tail_chunk);
+                size = A.tail_chunk;
+              }
+            }
           } else {
             size = A.prio_chunk;
           }

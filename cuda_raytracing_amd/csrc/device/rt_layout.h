@@ -273,6 +273,8 @@ struct RenderArgs {
   uint32_t mix_no_proof;          // test aid (RT_MIX_PROVE=0): every macro walk takes the fallback
   uint32_t tail_prio;             // queue drained: a wave's issue priority grows with the samples its least
                                   // advanced pixel has left (the frame ends with its longest chain)
+  uint32_t tail_ids, tail_chunk;  // the last tail_ids ids of the order (a multiple of 64; 0 = none) are handed out in
+                                  // pieces of tail_chunk (a power of two < 64) from work[kTailWord]
   // kernel-only timing (non-null on the render launch): span[0] = max over waves of ~start, span[1] = max of
   // end, s_memrealtime ticks (the device's wall clock) — the launch's first wave start to its last wave end,
   // like a profiler's kernel duration and unlike stream events, never widened by neighbouring work
@@ -293,6 +295,7 @@ enum : uint32_t { kStageDone = 192, kStageTile = 194, kStageValid = 196 };
 constexpr uint32_t kStageFree = 0xffffffffu;
 constexpr uint32_t kStageSlotsMax = 4;
 constexpr uint32_t kXcdClasses = 8, kClsWord = 36;   // (work words 16..35: the mixed walk's RT_MIX_DIAG counters)
+constexpr uint32_t kTailWord = 44;                   // work word of the tail pieces' counter
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)

@@ -307,6 +307,9 @@ struct rt_context {
   uint32_t tile_shift = 3;         // (tile_shift_setting)
   int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
+  int tail_chunk = 0;              // RT_TAIL_CHUNK: the tail of the order in pieces of this many pixels (0: whole tiles)
+  double tail_gen = 1.0;           // RT_TAIL_GEN: ... over this many times the grid's lanes of ids
+  uint32_t used_tail_ids = 0;      // the last render's
   int rc_pool = 0;                 // deep-level pool chunks per wave (rc_pool_setting)
   bool rc_pool_set = false;        // ... given explicitly: also for shallow kernels
   uint32_t used_pool_chunks = 0;   // the last render's
@@ -513,6 +516,11 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
   if (const char *e = std::getenv("RT_XCD_CLASSES")) c->xcd_classes = e[0] == '1';
   c->stage_slots = stage_slots_setting();
   c->rc_pool = rc_pool_setting(&c->rc_pool_set);
+  if (const char *e = std::getenv("RT_TAIL_CHUNK")) {
+    const int v = std::atoi(e);
+    c->tail_chunk = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
+  }
+  if (const char *e = std::getenv("RT_TAIL_GEN")) c->tail_gen = std::max(0.0, std::atof(e));
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     c->accel_lds_set = true;
@@ -1174,7 +1182,22 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // Tail issue priority: on for the verified mixed walk (final_scene 800x800 spp 64: 638-649 -> 598-611 ms
   // per frame), within noise elsewhere (scene 0 -1 %, 10k +1 %; profiles/r03_ab_tail_prio.jsonl)
   a.tail_prio = (c->tail_prio == 1 || (c->tail_prio < 0 && c->used_traversal == RT_TRAV_MIXED)) ? 1u : 0u;
-  if (std::getenv("RT_DEBUG") && c->used_lpt) std::fprintf(stderr, "[rt] tile queues: %s\n", a.cls_off ? "8 XCD classes" : "one");
+  // Tail pieces (RT_TAIL_CHUNK, RT_TAIL_GEN): the last tail_gen x (grid lanes) ids of the longest-first order go out in
+  // tail_chunk-pixel pieces, so that a wave holds few pixels it has not started when the queue drains (whole tiles: up
+  // to 63), and the waves' last pixels start closer together.  Longest-first order only, whole-tile queues.
+  a.tail_ids = 0u;
+  a.tail_chunk = 0u;
+  if (c->used_lpt && !a.cls_off && c->tail_chunk > 0) {
+    const uint32_t prio_lo = a.prio_chunk < 64u ? a.prio_ids : 0u;   // split costliest ids come first, never in the tail
+    const double want = c->tail_gen * static_cast<double>(threads);
+    const uint32_t room = (a.n_ids - std::min(a.n_ids, (prio_lo + 63u) / 64u * 64u)) / 64u * 64u;
+    a.tail_ids = std::min<uint32_t>(room, static_cast<uint32_t>(std::max(0.0, want) / 64.0) * 64u);
+    a.tail_chunk = a.tail_ids ? static_cast<uint32_t>(c->tail_chunk) : 0u;
+  }
+  c->used_tail_ids = a.tail_ids;
+  if (std::getenv("RT_DEBUG") && c->used_lpt)
+    std::fprintf(stderr, "[rt] tile queues: %s, tail pieces: %u ids in %u-pixel pieces\n", a.cls_off ? "8 XCD classes" : "one",
+                 a.tail_ids, a.tail_chunk);
   a.span = reinterpret_cast<unsigned long long *>(static_cast<uint32_t *>(c->work.p) + kSpanWord);   // zeroed above
   if (hipEventRecord(c->ev[3], s) != hipSuccess) return RT_ERR_HIP;
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)

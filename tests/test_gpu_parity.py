@@ -241,6 +241,23 @@ def test_tail_issue_priority_agrees(idx, W, H, spp, tail, monkeypatch):
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
 
 
+@pytest.mark.parametrize("idx,W,H,spp", [(0, 96, 54, 24), (20, 64, 36, 16), (3, 48, 48, 16), (17, 64, 36, 16)])
+@pytest.mark.parametrize("chunk,gen", [("1", "1"), ("8", "0.5"), ("32", "4")])
+def test_tail_pieces_agree(idx, W, H, spp, chunk, gen, monkeypatch):
+    # RT_TAIL_CHUNK hands the last ids of the longest-first order out in pieces of 1..32 pixels from their own
+    # counter (seeded per piece at pickup): which lane renders a pixel changes, the frame must not — with whole tiles
+    # before (scene 0, 10k), split costliest tiles and sparse hot waves (Perlin), mixed hot waves (final_scene); at
+    # these sizes the tail covers part of the frame (gen 0.5) or all of it (gen 4)
+    monkeypatch.setenv("RT_TAIL_CHUNK", chunk)
+    monkeypatch.setenv("RT_TAIL_GEN", gen)
+    w, s = rt.build_scene(idx)
+    cam, W, H = rt.camera_from_settings(s, W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=16)
+    fb, _ = gpu(w.scene(), cam, p)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and np.array_equal(bits(fb), bits(ref))
+
+
 @pytest.mark.parametrize("idx", [0, 1, 2, 8, 13, 18, 19])
 def test_folded_and_unfolded_static_traversal(idx):
     # exact constant folding of primitive tests (scene_codegen.cpp) must not change a single bit
