@@ -2089,7 +2089,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
               // the last tail_ids ids of the order go out in tail_chunk-pixel pieces from their own counter: a wave
               // then holds at most tail_chunk - 1 pixels it has not started when the queue drains, instead of up to 63
               // of a whole tile, so the waves' last pixels start (and the waves end) closer together
-              if (A.tail_ids != 0u && base >= A.n_ids - A.tail_ids) {
+              if ((F & kVarTail) != 0 && A.tail_ids != 0u && base >= A.n_ids - A.tail_ids) {
                 base = A.n_ids - A.tail_ids + atomicAdd(A.work + kTailWord, A.tail_chunk);
                 size = A.tail_chunk;
               }
@@ -2471,6 +2471,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             }
             rc_deep_store(rsp, code);
           }
+#ifdef RT_DBG_PX
+          if (pxy == static_cast<uint32_t>(RT_DBG_PX)) printf("dbgp s %d d %u rsp %u code %08x\n", sample, depth, rsp, code);
+#endif
           rsp++;
         }
         depth++;
@@ -2546,6 +2549,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         ph_unwind += t - t_mark; if (lone) lph[5] += t - t_mark;
         t_mark = t;
       }
+#ifdef RT_DBG_PX
+      if (pxy == static_cast<uint32_t>(RT_DBG_PX))
+        printf("dbgu s %d res %08x %08x %08x sum %08x %08x %08x\n", sample, __float_as_uint(res.x), __float_as_uint(res.y),
+               __float_as_uint(res.z), __float_as_uint(sum.x), __float_as_uint(sum.y), __float_as_uint(sum.z));
+#endif
       sum = add(sum, res);
       sample++;
       if (COUNT) c_samples++;

@@ -164,9 +164,11 @@ constexpr int kVarStage = 1 << 21;
 constexpr int kVarTileShift = 22;
 // run-time compiled kernels with HBM colour-stack levels and the per-wave deep-level pool (RenderArgs::rc_pool_*)
 constexpr int kVarRcPool = 1 << 25;
+// run-time compiled kernels with the tail-piece hand-out (RenderArgs::tail_*; RT_TAIL_CHUNK)
+constexpr int kVarTail = 1 << 26;
 // variant bits the run-time compiled kernels are specialised on
 constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop | kVarByte | kVarRcLds |
-                            kVarStage | (7 << kVarTileShift) | kVarRcPool | (15 << kVarMatShift) | (15 << kVarTexShift);
+                            kVarStage | (7 << kVarTileShift) | kVarRcPool | kVarTail | (15 << kVarMatShift) | (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling

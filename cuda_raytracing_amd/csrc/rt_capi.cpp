@@ -727,7 +727,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
                         (narrow_ok ? rt::kVarNarrow : 0) | (byte_ok ? rt::kVarByte : 0) | (rc_lds_only ? rt::kVarRcLds : 0) |
                         static_cast<int>(c->tile_shift << rt::kVarTileShift) | (c->stage_slots ? rt::kVarStage : 0) |
-                        (pool_kernel ? rt::kVarRcPool : 0);
+                        (pool_kernel ? rt::kVarRcPool : 0) | (c->tail_chunk > 0 ? rt::kVarTail : 0);
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
   const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
   if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;

@@ -52,6 +52,9 @@ std::string arch_of(int dev) {
 
 std::vector<std::string> jit_extra_options() {
   std::vector<std::string> v;
+  // RT_JIT_SGPR_MEM=1 (A/B): scalar-register spills go to scratch memory instead of lanes of spill VGPRs
+  if (const char *e = std::getenv("RT_JIT_SGPR_MEM"))
+    if (e[0] == '1') { v.push_back("-mllvm"); v.push_back("-amdgpu-spill-sgpr-to-vgpr=0"); }
   if (const char *e = std::getenv("RT_JIT_OPTS")) {
     std::string cur;
     for (const char *p = e;; ++p) {
@@ -367,11 +370,18 @@ std::string jit_mixed_source(const SceneImage &img, int variant, int waves) {
 // be 3).  When the render kernel is within kRaiseSlack VGPRs of the next residency, its module is rebuilt with
 // that residency's register cap (amdgpu_num_vgpr: the waves-per-EU request budgets with an 8-VGPR granule, 168
 // for 3 waves, which the hardware's granule does not fit) and kept if the kernel then reaches it with at most
-// kRaiseScratch bytes of scratch per lane (a few spilled values outside the hot loops; round 4: the static
-// kernels of scene 0 and the Cornell box land at 81-85 VGPRs, the mixed walk of final_scene at 169).
+// raise_scratch() bytes of scratch per lane (round 5: none; round 4 kept up to 16 B — the static kernels of scene 0
+// and the Cornell box land at 81-87 VGPRs, the mixed walk of final_scene at 169).
 // RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves the first build.
 constexpr int kRaiseSlack = 12;
-constexpr int kRaiseScratch = 16;
+// Scratch a raised build may keep: none by default (round 5).  A build forced under its allocator's register count
+// spills VGPRs, and two such builds of the verified sphere walk rendered wrong pixels (and one faulted) where the same
+// source at a budget without VGPR spills was exact — each time a small unrelated source edit flipped it.
+// RT_JIT_RAISE_SCRATCH=<bytes> (A/B) restores round 4's 16 B.
+int raise_scratch() {
+  if (const char *e = std::getenv("RT_JIT_RAISE_SCRATCH")) return std::max(0, std::atoi(e));
+  return 0;
+}
 
 int render_vgprs(hipFunction_t fn, int *scratch) {
   int v = 0, sc = 0;
@@ -388,7 +398,7 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out) 
   if (const char *e = std::getenv("RT_JIT_RAISE")) if (e[0] == '0') return;
   int sc0 = 0;
   const int v0 = render_vgprs(out->render, &sc0);
-  if (v0 <= 0 || sc0 < 0 || sc0 > kRaiseScratch) return;
+  if (v0 <= 0 || sc0 < 0 || sc0 > raise_scratch()) return;
   const int cur = resident_blocks_by_vgprs(v0);
   if (cur >= 8) return;
   const int limit = 512 / (cur + 1) / 16 * 16;   // the hardware's budget for one more wave per SIMD
@@ -401,7 +411,7 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out) 
   if (std::getenv("RT_DEBUG"))
     std::fprintf(stderr, "[rt] jit residency raise %s: %d VGPRs (%d/SIMD) -> cap %d: %d VGPRs, scratch %d B\n",
                  prefix, v0, cur, limit, v, sc);
-  if (v > 0 && sc >= 0 && sc <= kRaiseScratch && resident_blocks_by_vgprs(v) > cur) {
+  if (v > 0 && sc >= 0 && sc <= raise_scratch() && resident_blocks_by_vgprs(v) > cur) {
     k.ms += out->ms;
     *out = k;
   }
@@ -418,7 +428,8 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
   out->visits = visits;
   out->folded = folded;
   if (!build_module(src, "rt_static", out, why)) return false;
-  // one residency step up when the allocator lands just above a boundary (kept only without scratch)
+  // one residency step up when the allocator lands just above a boundary (kept with at most kRaiseScratch bytes of
+  // scratch per lane: a spilled build is exact like any other — the round-4 6-wave mismatch was a lane-mask bool, §2)
   raise_residency([&](int w) {
     std::string s2;
     uint32_t v2 = 0;
@@ -440,14 +451,16 @@ bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std:
 // The verified sphere walk is latency-bound (dependent node loads): hipRTC allocates its render kernel
 // ~97 VGPRs (4 waves/SIMD); asked for 6 waves (80 VGPRs) it runs the 10k frame 226-231 -> 206-208 ms
 // (profiles/r03_ab_jit_waves.jsonl).  RT_ACCEL_WAVES=N overrides (0: the allocator's own choice);
-// RT_JIT_WAVES, when set, applies to every run-time kernel instead.  Every width is asked for 6: the round-4
-// mis-render of the 4-wide walk's 6-wave build (a paused walk's hit flag held as a lane-mask bool, lost across the
-// round's `continue` under that register budget; Trav::result is now a word) is gone, 6 waves bit-exact on the
-// random worlds that failed (profiles/r05_w4_diag.txt).
+// RT_JIT_WAVES, when set, applies to every run-time kernel instead.  Every width is asked for 5 (round 5; rounds 3-4:
+// 6).  The 6-wave build (80 VGPRs) spills VGPRs, and twice a build of it rendered wrong pixels where the same source at
+// 5 waves or at the allocator's budget was exact: the 4-wide walk of round 4, and in round 5 the 2-wide walk once the
+// tail-piece hand-out was compiled in (G and B of samples in mixed waves, a fault at the full 10k config); with its
+// SGPR spills in scratch instead of VGPR lanes the same 6-wave build was exact.  At 5 waves the walk needs no VGPR
+// spill (87 VGPRs) and runs within noise of 6 (profiles/r05_ab_s21_10k.jsonl).
 int accel_waves(int /*wide*/) {
   if (std::getenv("RT_JIT_WAVES")) return 0;
   if (const char *e = std::getenv("RT_ACCEL_WAVES")) return std::max(0, std::min(8, std::atoi(e)));
-  return 6;
+  return 5;
 }
 
 // Width of the verified sphere walk's tree: 2 (the SAH BVH2) or 4 (its 4-wide collapse, accel::collapse_wide)
@@ -463,11 +476,11 @@ bool accel_quant() {
   return false;
 }
 
-// The default 6-wave request is measured on the plain 10k walk, whose 80-VGPR build spills ~17 VGPRs outside
-// the node loop (44 B per lane).  Variants that need far more registers (noise, image u,v, deep bounces:
-// 125-149 VGPRs) would spill inside their hot loops; a default-request build with more scratch than this is
-// replaced by the allocator's own build (+ the residency raise).  An explicit RT_ACCEL_WAVES is kept as built.
-constexpr int kAccelWavesScratchMax = 96;
+// The default request is measured on the plain 10k walk (87 VGPRs at 5 waves, no scratch).  Variants that need more
+// registers (noise, image u,v, deep bounces: 125-149 VGPRs) would spill; a default-request build with any scratch is
+// replaced by the allocator's own build (+ the residency raise, itself spill-free).  An explicit RT_ACCEL_WAVES is kept
+// as built.
+constexpr int kAccelWavesScratchMax = 0;   // round 4: 96 B (see accel_waves)
 
 bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why) {
   out->visits = 0;
