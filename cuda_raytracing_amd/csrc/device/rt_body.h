@@ -1881,18 +1881,26 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   // is wave-private (taken at the push, returned by LDS atomics at the unwind, program-ordered within the wave)
   constexpr bool POOL = !RC_LDS && (F & kVarRcPool) != 0;
   const uint32_t pool_stride = mb > A.rc_lds_levels ? mb - A.rc_lds_levels : 0u;
-  uint32_t *const pool = g_lds + __builtin_amdgcn_readfirstlane(A.rc_pool_word + wave * (1u + A.rc_pool_chunks * pool_stride));
-  uint32_t pc = kRcNoChunk;   // the lane's chunk for its current path's deep levels
+  uint32_t *const pool = g_lds + __builtin_amdgcn_readfirstlane(A.rc_pool_word + wave * (kRcPoolHead + A.rc_pool_chunks * pool_stride));
+  // the lane's chunk (0xff: none) in a byte of the wave's pool header, not in a register carried through the traversal
+  uint8_t *const pool_lane = reinterpret_cast<uint8_t *>(pool + 1) + lane;
   if (POOL) {
     if (lane == 0) pool[0] = A.rc_pool_chunks >= 32u ? 0xffffffffu : (1u << A.rc_pool_chunks) - 1u;
+    *pool_lane = 0xffu;
     __threadfence_block();
   }
   auto rc_deep_store = [&](uint32_t k, uint32_t code) {
-    if (POOL && pc != kRcNoChunk) pool[1u + pc * pool_stride + (k - A.rc_lds_levels)] = code;
-    else rc_hbm_store(k, code);
+    if constexpr (POOL) {
+      const uint32_t c = *pool_lane;
+      if (c != 0xffu) { pool[kRcPoolHead + c * pool_stride + (k - A.rc_lds_levels)] = code; return; }
+    }
+    rc_hbm_store(k, code);
   };
   auto rc_deep_load = [&](uint32_t k) -> uint32_t {
-    if (POOL && pc != kRcNoChunk) return pool[1u + pc * pool_stride + (k - A.rc_lds_levels)];
+    if constexpr (POOL) {
+      const uint32_t c = *pool_lane;
+      if (c != 0xffu) return pool[kRcPoolHead + c * pool_stride + (k - A.rc_lds_levels)];
+    }
     return rc_hbm_load(k);
   };
 
@@ -2449,24 +2457,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
               const bool first = rsp == A.rc_lds_levels;
               const uint64_t need = __ballot(first);
               if (need != 0) {
-                const uint32_t fm = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(pool[0]));
-                const uint32_t nfree = static_cast<uint32_t>(__popc(fm));
-                const uint32_t take = min(static_cast<uint32_t>(__popcll(need)), nfree);
-                if (first) {
-                  uint32_t r = static_cast<uint32_t>(__popcll(need & lt_mask));
-                  if (r < nfree) {   // the r-th set bit of fm
-                    uint32_t pos = 0;
-#pragma unroll
-                    for (uint32_t s = 16; s >= 1; s >>= 1) {
-                      const uint32_t c = static_cast<uint32_t>(__popc((fm >> pos) & ((1u << s) - 1u)));
-                      if (r >= c) { r -= c; pos += s; }
-                    }
-                    pc = pos;
-                  }
+                // scalar loop over the needing lanes (few per round): lane l takes the lowest free chunk
+                uint32_t fm = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(pool[0]));
+                uint64_t nm = need;
+                while (nm != 0 && fm != 0) {
+                  const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(nm));
+                  if (lane == l) *pool_lane = static_cast<uint8_t>(__builtin_ctz(fm));
+                  nm &= nm - 1ull;
+                  fm &= fm - 1u;
                 }
-                uint32_t left = fm;
-                for (uint32_t i = 0; i < take; ++i) left &= left - 1u;   // wave-uniform
-                pool[0] = left;   // (every active lane stores the same word)
+                pool[0] = fm;   // (every active lane stores the same word)
               }
             }
             rc_deep_store(rsp, code);
@@ -2501,6 +2501,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
       // The "+ 0.0f" of each level only turns a -0 into +0 (an underflowed product stays +-0 in every
       // later level) and sum = +0 + ... is never -0, so it is dropped (the pixel is bit-identical); the
       // same argument covers the dielectric levels, which are not pushed (att (1,1,1)).
+      const bool rsp_deep = POOL && rsp > A.rc_lds_levels;   // the path pushed past its LDS levels
       if (A.black_skip && rsp > 0 && res.x == 0.0f && res.y == 0.0f && res.z == 0.0f) {
         res = mk(0.0f, 0.0f, 0.0f);
         rsp = 0;
@@ -2538,10 +2539,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           res = mk(at[i].x * res.x, at[i].y * res.y, at[i].z * res.z);
         }
       }
-      if constexpr (POOL) {   // the path's pool chunk (read above, or skipped with a black path) is free again
-        if (pc != kRcNoChunk) {
-          atomicOr(pool, 1u << pc);
-          pc = kRcNoChunk;
+      if constexpr (POOL) {   // a deep path's pool chunk (read above, or skipped with a black path) is free again
+        if (rsp_deep) {
+          const uint32_t c = *pool_lane;
+          if (c != 0xffu) {
+            atomicOr(pool, 1u << c);
+            *pool_lane = 0xffu;
+          }
         }
       }
       if (TRACE) {   // the unwind's share of the done block (the rest: camera ray / pixel write)

@@ -192,9 +192,10 @@ struct RenderArgs {
   uint32_t off_mats, off_texs, off_perlin, off_pixels, pixel_words;
   uint32_t root, stack_cap, stack_lds_word;   // per-lane stack region starts at this LDS word
   uint32_t rc_lds_word, rc_lds_levels;        // colour-stack levels [0, rc_lds_levels) live in LDS
-  // Deep-level pool (kVarRcPool kernels): per wave, from LDS word rc_pool_word + wave * (1 + rc_pool_chunks * (max_bounces
-  // - rc_lds_levels)), a free-chunk mask word, then rc_pool_chunks chunks of max_bounces - rc_lds_levels words.  A path's
-  // levels past the LDS ones go to a chunk when one is free at its first such push, else to HBM (rc)
+  // Deep-level pool (kVarRcPool kernels): per wave, from LDS word rc_pool_word + wave * (kRcPoolHead + rc_pool_chunks *
+  // (max_bounces - rc_lds_levels)), a free-chunk mask word, the lanes' chunk bytes (16 words), then rc_pool_chunks chunks
+  // of max_bounces - rc_lds_levels words.  A path's levels past the LDS ones go to a chunk when one is free at its first
+  // such push, else to HBM (rc)
   uint32_t rc_pool_word, rc_pool_chunks;
   uint32_t rc_tex0, rc_consts;                // colour records: first texture, first constant
   // camera (rt_camera)
@@ -302,7 +303,7 @@ constexpr uint32_t kTailWord = 44;                   // work word of the tail pi
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)
 constexpr uint32_t kRcPoolChunksMax = 32;   // deep-level pool chunks per wave (one mask word)
-constexpr uint32_t kRcNoChunk = 0xffffffffu;
+constexpr uint32_t kRcPoolHead = 17;         // per wave: the free-chunk mask word, then each lane's chunk byte (16 words)
 
 struct SeedArgs {
   const uint32_t *jump;       // xorwow_jump_tables() on device

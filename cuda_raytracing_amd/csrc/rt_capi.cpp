@@ -118,7 +118,7 @@ constexpr size_t kStageWaveExtraBytes = static_cast<size_t>(rt::kWavesPerBlock) 
 constexpr size_t kRcLdsOnlyBlocks = 6;      // LDS-only colour stacks (kVarRcLds) must fit this many blocks per CU
 constexpr uint32_t kDefaultTileShift = 3;    // 8x8 tiles
 constexpr uint32_t kDefaultStageSlots = 0;   // pixels stored when they end
-constexpr int kDefaultRcPool = 0;            // deep-level pool chunks per wave of deep kernels with HBM levels (RT_RC_POOL)
+constexpr int kDefaultRcPool = 8;            // deep-level pool chunks per wave of deep kernels with HBM levels (RT_RC_POOL)
 constexpr int kPrioTiles = 256;                 // costliest tiles at raised issue priority (RT_PRIO_TILES)
 constexpr int kSparseLanes = 2;                 // noise scenes: busy lanes per wave holding the costliest pixels
 constexpr int kSparseTiles = 16;                // ... over this many costliest tiles (RT_PRIO_LANES / _TILES)
@@ -894,7 +894,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     const size_t fixed = c->lds_bytes - rc_levels * level_bytes;   // scene (or SAH top nodes), stacks, RNG slots
     const size_t cap = kLdsPerCu / static_cast<size_t>(std::max(per_cu, 1)) - kLdsReserve;
     auto bytes_of = [&](uint32_t P, uint32_t L) {
-      return static_cast<size_t>(rt::kWavesPerBlock) * (1u + P * (mb > L ? mb - L : 0u)) * 4u;
+      return static_cast<size_t>(rt::kWavesPerBlock) * (rt::kRcPoolHead + P * (mb > L ? mb - L : 0u)) * 4u;
     };
     const uint32_t min_levels = std::max<uint32_t>(c->rc_lds_levels, codes_per_word);
     uint32_t L = rc_levels;
@@ -910,7 +910,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     }
     rc_levels = L;
     pool_base = fixed + rc_levels * level_bytes;
-    pool_bytes = bytes_of(pool_chunks, rc_levels);   // the mask words even without chunks (the kernel sets them)
+    pool_bytes = bytes_of(pool_chunks, rc_levels);   // the headers even without chunks (the kernel sets them)
     c->lds_bytes = pool_base + pool_bytes;
   }
   c->used_pool_chunks = pool_chunks;
