@@ -721,7 +721,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
   const bool rc_lds_only = c->rc_lds_auto && !c->rc_lds_only_off && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
   // the deep-level pool's code in run-time kernels with HBM levels (sized below, once the residency is known)
-  const bool pool_kernel = c->rc_pool > 0 && !rc_lds_only && (mb > static_cast<uint32_t>(rt::kDeepBounces) || c->rc_pool_set);
+  // (by default deep kernels with automatic levels; pinned levels, RT_RC_LDS_LEVELS, get one only with RT_RC_POOL)
+  const bool pool_kernel = c->rc_pool > 0 && !rc_lds_only &&
+                           (c->rc_pool_set || (c->rc_lds_auto && mb > static_cast<uint32_t>(rt::kDeepBounces)));
   // run-time compiled kernels only: diagnostics timeline + the scene's material/texture kinds
   const int trace_bit = (c->wave_trace_path.empty() ? 0 : rt::kVarTrace) | (c->shade_spec ? rt::scene_shading_bits(c->img) : 0) |
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |

@@ -24,3 +24,4 @@ run 1 1920 1080 1024 50
 run 17 1920 1080 1024 50
 run 20 1920 1080 256 16
 run 0 3840 2160 2048 50
+run 3 800 800 64 40
