@@ -22,7 +22,10 @@
 #define RT_UNWIND_LDS 3     // LDS colour-stack levels loaded per batch in the unwind
 #endif
 #ifndef RT_UNWIND_LDS_DEEP
-#define RT_UNWIND_LDS_DEEP 8   // ... in deep-path kernels (max_bounces > kDeepBounces)
+// ... in deep-path kernels (max_bounces > kDeepBounces).  5 since round 5: the Cornell and 4K scene-0 d50 kernels then
+// fit 80 VGPRs (6 waves) without spilling (8: 87 VGPRs, 5 waves); same box: Cornell -4.5 %, 4K -7 %, Perlin level
+// (profiles/r05_ab_s29_*.jsonl)
+#define RT_UNWIND_LDS_DEEP 5
 #endif
 
 namespace rt {
