@@ -832,8 +832,9 @@ def test_colour_stack_pool_automatic_levels(idx, W, H, spp, monkeypatch):
     (fb0, st0), _, _ = _pool_render(w, s, W, H, spp, 50, 0, 0, monkeypatch)
     (fb, st), _, _ = _pool_render(w, s, W, H, spp, 50, 0, 16, monkeypatch)
     assert np.array_equal(bits(fb0), bits(ref)) and np.array_equal(bits(fb), bits(ref))
-    if st0.rc_lds_levels < 50:   # a kernel with HBM levels: the pool is used, levels give way to it
-        assert st.rc_pool_chunks > 0 and st.rc_lds_levels <= st0.rc_lds_levels
+    if st0.rc_lds_levels < 50:   # a kernel with HBM levels: the pool is used (its per-lane levels follow the pool
+        # kernel's own residency, which may differ) and keeps levels out of HBM
+        assert st.rc_pool_chunks > 0
         assert st.rc_hbm_slots <= st0.rc_hbm_slots
 
 
