@@ -2586,6 +2586,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           const uint64_t was = atomicOr(reinterpret_cast<unsigned long long *>(sq + kStageDone), 1ull << k);
           if (((was | (1ull << k)) & all) == all)   // the tile's last pixel: the wave stores it next round
             atomicOr(stage_done, 1u << static_cast<uint32_t>((sq - stage) / kStageSlotWords));
+        } else if constexpr ((F & kVarTiledOut) != 0) {   // tile-major frame (untile_kernel writes rows and bytes)
+          const uint32_t tile = (plr >> tsh) * A.tiles_x + (pj >> ts);
+          const uint32_t k = ((plr & ((1u << tsh) - 1u)) << ts) | (pj & twm);
+          float *o = A.out + static_cast<size_t>(tile) * 192u + 3u * k;
+          o[0] = c.x;
+          o[1] = c.y;
+          o[2] = c.z;
         } else {
           const size_t pix = static_cast<size_t>(plr) * static_cast<uint32_t>(A.width) + pj;
           float *o = A.out + 3 * pix;

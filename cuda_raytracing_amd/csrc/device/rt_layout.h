@@ -166,9 +166,13 @@ constexpr int kVarTileShift = 22;
 constexpr int kVarRcPool = 1 << 25;
 // run-time compiled kernels with the tail-piece hand-out (RenderArgs::tail_*; RT_TAIL_CHUNK)
 constexpr int kVarTail = 1 << 26;
+// run-time compiled kernels that write the float frame tile-major (RenderArgs::out: tile t's 64 pixels x 3 floats at
+// 192 t, pixel k of the tile at 3 k), so that every 128-B line of it is written by one wave through one XCD's L2; the
+// row-major frame and the PPM bytes come from untile_kernel after the render (RT_TILED_OUT)
+constexpr int kVarTiledOut = 1 << 27;
 // variant bits the run-time compiled kernels are specialised on
 constexpr int kJitVarMask = kVarLds | kVarNoise | kVarUv | kVarTrace | kVarDeep | kVarNarrow | kVarCoop | kVarByte | kVarRcLds |
-                            kVarStage | (7 << kVarTileShift) | kVarRcPool | kVarTail | (15 << kVarMatShift) | (15 << kVarTexShift);
+                            kVarStage | (7 << kVarTileShift) | kVarRcPool | kVarTail | kVarTiledOut | (15 << kVarMatShift) | (15 << kVarTexShift);
 
 // per wave: start, end (s_memrealtime), tiles, hw ids, rounds, busy lane-rounds, s_memtime cycles in
 // refill / traversal / unwind+accumulate+next camera ray / material scatter / rejection sampling

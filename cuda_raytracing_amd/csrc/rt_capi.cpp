@@ -245,6 +245,7 @@ struct rt_context {
   bool mix_no_proof = false;   // RT_MIX_PROVE=0 (test aid): every macro walk falls back
   int static_ok = -1;          // the scene expands within jit_budget (straight-line, stackless traversal); -1 unknown
   DevBuf scene, jump, rng_rows, rng_cols, rc, work, counters, wave_trace, tile_cost, tile_order, prim_lists, prim_counts;
+  DevBuf tiled;                    // tile-major render output (RT_TILED_OUT)
   // seeding tables of the last geometry, kept on the device: the phase bases (xorwow_phase_bases; key = seed, W,
   // rows of the shard) and the column tables (xorwow_column_tables; key = W)
   uint64_t rows_key[5] = {~0ull, 0, 0, 0, 0};
@@ -307,6 +308,8 @@ struct rt_context {
   uint32_t tile_shift = 3;         // (tile_shift_setting)
   int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
+  bool tiled_out = false;          // RT_TILED_OUT=1: the render writes the frame tile-major, untile_kernel the rows + bytes
+  bool used_tiled = false;         // the last render's
   int tail_chunk = 0;              // RT_TAIL_CHUNK: the tail of the order in pieces of this many pixels (0: whole tiles)
   double tail_gen = 1.0;           // RT_TAIL_GEN: ... over this many times the grid's lanes of ids
   uint32_t used_tail_ids = 0;      // the last render's
@@ -466,7 +469,7 @@ void rt_context_destroy(rt_context *c) {
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
     c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->prim_lists.release(); c->prim_counts.release(); c->rc.release();
     c->work.release(); c->counters.release();
-    c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release();
+    c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release(); c->tiled.release();
     c->rows_stage.release(); c->cols_stage.release();
   }
   delete c;
@@ -521,6 +524,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->tail_chunk = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
   }
   if (const char *e = std::getenv("RT_TAIL_GEN")) c->tail_gen = std::max(0.0, std::atof(e));
+  if (const char *e = std::getenv("RT_TILED_OUT")) c->tiled_out = e[0] == '1';
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     c->accel_lds_set = true;
@@ -720,6 +724,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
   const bool rc_lds_only = c->rc_lds_auto && !c->rc_lds_only_off && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
+  // tile-major output (run-time kernels; not with output staging, which stores whole tiles row-major itself)
+  const bool tiled_kernel = c->tiled_out && c->stage_slots == 0 && out_dev != nullptr;
   // the deep-level pool's code in run-time kernels with HBM levels (sized below, once the residency is known)
   // (by default deep kernels with automatic levels; pinned levels, RT_RC_LDS_LEVELS, get one only with RT_RC_POOL)
   const bool pool_kernel = c->rc_pool > 0 && !rc_lds_only &&
@@ -729,7 +735,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                         (mb > static_cast<uint32_t>(rt::kDeepBounces) ? rt::kVarDeep : 0) |
                         (narrow_ok ? rt::kVarNarrow : 0) | (byte_ok ? rt::kVarByte : 0) | (rc_lds_only ? rt::kVarRcLds : 0) |
                         static_cast<int>(c->tile_shift << rt::kVarTileShift) | (c->stage_slots ? rt::kVarStage : 0) |
-                        (pool_kernel ? rt::kVarRcPool : 0) | (c->tail_chunk > 0 ? rt::kVarTail : 0);
+                        (pool_kernel ? rt::kVarRcPool : 0) | (c->tail_chunk > 0 ? rt::kVarTail : 0) |
+                        (tiled_kernel ? rt::kVarTiledOut : 0);
   const bool accel_allowed = c->accel_ok && !(p->flags & RT_FLAG_NO_ACCEL) && !(p->flags & RT_FLAG_NO_JIT);
   const bool mixed_allowed = c->mixed_ok && !(p->flags & RT_FLAG_NO_MIXED) && !(p->flags & RT_FLAG_NO_JIT);
   if (trav == RT_TRAV_ACCEL && !accel_allowed) trav = mixed_allowed && (p->flags & RT_FLAG_FORCE_ACCEL) ? RT_TRAV_MIXED : RT_TRAV_LANE;
@@ -1045,8 +1052,13 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.rng_nib = static_cast<const uint32_t *>(c->rng_cols.p);
   a.rng_d = seed_base[0];
   a.rng_slot_word = scene_lds_words + rc_lds_words + static_cast<uint32_t>((stack_bytes - kRngSlotBytes) / 4);
-  a.out = out_dev;
-  a.out8 = out8_dev;
+  // tile-major output: the render kernel (a run-time kernel built with kVarTiledOut) writes the float frame tile by tile
+  // into c->tiled; untile_kernel then writes the caller's row-major floats and the PPM bytes (after the render, below)
+  const bool tiled = tiled_kernel && jit_fn != nullptr;
+  c->used_tiled = tiled;
+  if (tiled && c->tiled.ensure(static_cast<size_t>(n_ids) * 3u * 4u) != hipSuccess) return RT_ERR_HIP;
+  a.out = tiled ? static_cast<float *>(c->tiled.p) : out_dev;
+  a.out8 = tiled ? nullptr : out8_dev;
   a.rc = c->rc.p;
   a.threads = threads;
   a.work = static_cast<uint32_t *>(c->work.p);
@@ -1205,6 +1217,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
   if (le != hipSuccess) return RT_ERR_HIP;
+  if (tiled && rt::launch_untile(static_cast<const float *>(c->tiled.p), out_dev, out8_dev, static_cast<uint32_t>(p->row_count),
+                                 static_cast<uint32_t>(p->width), tiles_x, tile_shift, s) != hipSuccess)
+    return RT_ERR_HIP;
   if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
   c->ev_recorded = true;
   c->last_cam = *cam;

@@ -185,6 +185,26 @@ __global__ __launch_bounds__(256) void tonemap_kernel(const float *__restrict__ 
   }
 }
 
+// Tile-major render output (kVarTiledOut) -> the row-major float frame and, fused, the PPM bytes of the same floats.
+// One thread per output float: the writes are contiguous, the reads gather 12-B pixels from 768-B tiles.
+__global__ __launch_bounds__(256) void untile_kernel(const float *__restrict__ tiled, float *__restrict__ out,
+                                                     uint8_t *__restrict__ out8, uint32_t rows, uint32_t width,
+                                                     uint32_t tiles_x, uint32_t ts) {
+  const uint64_t e = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  if (e >= static_cast<uint64_t>(rows) * width * 3u) return;
+  const uint32_t p = static_cast<uint32_t>(e / 3u), c = static_cast<uint32_t>(e - 3ull * p);
+  const uint32_t lr = p / width, j = p - lr * width, tsh = 6u - ts;
+  const uint32_t tile = (lr >> tsh) * tiles_x + (j >> ts);
+  const uint32_t k = ((lr & ((1u << tsh) - 1u)) << ts) | (j & ((1u << ts) - 1u));
+  const float v = tiled[static_cast<size_t>(tile) * 192u + 3u * k + c];
+  out[e] = v;
+  if (out8) {
+    const float g = v > 0 ? sqrtf(v) : 0.0f;
+    const float q = (g < 0.0f) ? 0.0f : ((g > 0.999f) ? 0.999f : g);
+    out8[e] = static_cast<uint8_t>(static_cast<uint32_t>(256 * q) & 0xffu);
+  }
+}
+
 // Multi-device frames (rt_multi.cpp): the root's gathered buffer holds n shards of max_rows rows each (shard g =
 // rows g, g + n, ... of the frame, RCCL gather order); frame row k is shard k % n, row k / n.  One block row per
 // frame row; 4-byte words when rows are word-sized, bytes otherwise.
@@ -296,6 +316,15 @@ hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t 
   const uint32_t bx = (per + 255) / 256 < 16 ? (per + 255) / 256 : 16;
   hipLaunchKernelGGL(unpermute_kernel, dim3(bx, rows < 65535u ? rows : 65535u), dim3(256), 0, s,
                      static_cast<const uint8_t *>(src), static_cast<uint8_t *>(dst), rows, n, max_rows, row_bytes);
+  return hipGetLastError();
+}
+
+hipError_t launch_untile(const float *tiled, float *out, uint8_t *out8, uint32_t rows, uint32_t width, uint32_t tiles_x,
+                         uint32_t ts, hipStream_t s) {
+  const uint64_t n = static_cast<uint64_t>(rows) * width * 3u;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(untile_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, tiled, out, out8, rows,
+                     width, tiles_x, ts);
   return hipGetLastError();
 }
 

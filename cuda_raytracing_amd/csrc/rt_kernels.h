@@ -14,6 +14,10 @@ constexpr uint32_t kPacketMaxNodes = 512;           // packet DFS only for scene
 hipError_t launch_seed(const SeedArgs &a, hipStream_t s);
 // pixels_to_ppm byte conversion of n floats (3 per pixel) on the device
 hipError_t launch_tonemap(const float *rgb, uint64_t n, uint8_t *out, hipStream_t s);
+// tile-major render output (kVarTiledOut: tile t at 192 t floats) -> row-major floats [rows][width][3] and, if out8,
+// the PPM bytes of the same floats
+hipError_t launch_untile(const float *tiled, float *out, uint8_t *out8, uint32_t rows, uint32_t width, uint32_t tiles_x,
+                         uint32_t ts, hipStream_t s);
 // longest-first order of n tiles from probe costs (single block)
 // tiles_x != 0: grouped into 8 XCD classes (128-pixel column groups of 8x8 tiles), longest-first within each;
 // order[n .. n + 8] = the classes' first positions and n (order must hold n + 9 words)
