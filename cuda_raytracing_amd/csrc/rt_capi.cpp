@@ -1409,6 +1409,8 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0) |
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0) |
                       static_cast<int>(tile_shift_setting() << rt::kVarTileShift) | (stage_slots_setting() ? rt::kVarStage : 0);
+  if (const char *e = std::getenv("RT_TILED_OUT"))
+    if (e[0] == '1' && !stage_slots_setting()) variant |= rt::kVarTiledOut;
   {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks), else the pool's code
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
     const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +
