@@ -775,7 +775,11 @@ struct LaneTraceK {
     if (!busy) return;
     if (!PAUSE || !T.active) {
       trav_reset(T, r);
-      stk[0] = static_cast<uint16_t>(A.root);
+      // the root through a scalar operand: under the verified walk's 80-VGPR budget the allocator otherwise kept this
+      // uniform value in a VGPR and spilled it to scratch (round 5)
+      uint32_t root = A.root;
+      asm volatile("" : "+s"(root));
+      stk[0] = static_cast<uint16_t>(root);
       T.sp = 1;
     }
     if (!PAUSE) {
@@ -1210,6 +1214,10 @@ struct AccelTraceK {
   // stack (dead from the end of the walk to the next trace) instead of a register: at this kernel's 80-VGPR budget the
   // allocator otherwise spilled it to scratch once per bounce (scratch stores reach HBM: 10k config)
   static constexpr bool kParkRandomTest = true;
+  // the pixel's running sum (used once per sample) waits in the kSumEntries top entries of the lane's stack, above the
+  // walk's (the host adds them to stack_cap): three registers fewer across the walk, which then fits 80 VGPRs (6 waves)
+  // without spilling (round 5: default builds never spill VGPRs)
+  static constexpr bool kParkSum = true;
   template <bool LDS, bool UV>
   __device__ __forceinline__ static void materialize(const Mem<LDS> &S, const RenderArgs &A, const Trav &T, const Ray &r,
                                                      Hit &h) {
@@ -1246,6 +1254,8 @@ template <class TR> __device__ constexpr auto prim_lists(int) -> decltype(TR::kP
 template <class TR> __device__ constexpr bool prim_lists(long) { return false; }
 template <class TR> __device__ constexpr auto park_random_test(int) -> decltype(TR::kParkRandomTest, bool()) { return TR::kParkRandomTest; }
 template <class TR> __device__ constexpr bool park_random_test(long) { return false; }
+template <class TR> __device__ constexpr auto park_sum(int) -> decltype(TR::kParkSum, bool()) { return TR::kParkSum; }
+template <class TR> __device__ constexpr bool park_sum(long) { return false; }
 
 // ---------------------------------------------------------------------------------------------
 // traversal policy 5: verified traversal of mixed worlds (mixed_accel.cpp)
@@ -1918,6 +1928,34 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   Ray ray;
   ray.o = mk(0, 0, 0); ray.d = mk(0, 0, 0); ray.time = 0;
   f3 sum = mk(0, 0, 0);
+  // kParkSum traces: the sum lives in the lane's stack entries stack_cap - kSumEntries .. stack_cap - 1 (u16 halves)
+  constexpr bool kParkS = park_sum<Trace>(0);
+  auto sum_put = [&](const f3 &v) {
+    if constexpr (kParkS) {
+      uint16_t *e = stk + (A.stack_cap - kSumEntries) * 64u;
+      const uint32_t w[3] = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z)};
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        e[(2 * i) * 64] = static_cast<uint16_t>(w[i]);
+        e[(2 * i + 1) * 64] = static_cast<uint16_t>(w[i] >> 16);
+      }
+      asm volatile("" ::: "memory");   // reloaded from LDS, not kept in registers
+    } else {
+      sum = v;
+    }
+  };
+  auto sum_get = [&]() -> f3 {
+    if constexpr (kParkS) {
+      const uint16_t *e = stk + (A.stack_cap - kSumEntries) * 64u;
+      float f[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        f[i] = __uint_as_float(static_cast<uint32_t>(e[(2 * i) * 64]) | (static_cast<uint32_t>(e[(2 * i + 1) * 64]) << 16));
+      return mk(f[0], f[1], f[2]);
+    } else {
+      return sum;
+    }
+  };
   Trav T;
   T.inv = mk(0, 0, 0); T.rcp = mk(0, 0, 0); T.tmax = 0; T.active = 0; T.anode = 0; T.abest = 0; T.atie = 0; T.asp = 0; T.sp = 0; T.tc = 0; T.yc = 0; T.was_last = 0; T.result = false;
   Hit h;
@@ -2235,7 +2273,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
             rng.x3 = rng_slot[192u + so];
             rng.x4 = rng_slot[256u + so];
           }
-          sum = mk(0, 0, 0);
+          sum_put(mk(0, 0, 0));
           sample = 0;
           camera_ray();
         }
@@ -2253,13 +2291,13 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     // SIMD's arbiter otherwise favours the oldest waves (measured: 20 vs 28 us per round, first vs third
     // wave of a SIMD on the 10k scene), so the level grows with the least advanced pixel's remaining share
     if (A.tail_prio && exhausted) {
-      int32_t rem = busy ? A.spp - sample : 0;
-#pragma unroll
-      for (int sh = 1; sh < 64; sh <<= 1) rem = max(rem, __shfl_xor(rem, sh));
-      const uint32_t lvl = 4u * static_cast<uint32_t>(rem) > 3u * static_cast<uint32_t>(A.spp) ? 3u
-                         : 2u * static_cast<uint32_t>(rem) > static_cast<uint32_t>(A.spp) ? 2u
-                         : 4u * static_cast<uint32_t>(rem) > static_cast<uint32_t>(A.spp) ? 1u : 0u;
-      want_prio = max(want_prio, __builtin_amdgcn_readfirstlane(lvl));
+      // the level of the wave's largest remaining share, by ballots (each threshold holds for the maximum iff it holds
+      // for some lane; no cross-lane shuffle, whose lane addresses the compiler would keep live across the loop)
+      const uint32_t rem = busy ? static_cast<uint32_t>(A.spp - sample) : 0u, spp = static_cast<uint32_t>(A.spp);
+      const uint32_t lvl = __ballot(4u * rem > 3u * spp) != 0 ? 3u
+                         : __ballot(2u * rem > spp) != 0 ? 2u
+                         : __ballot(4u * rem > spp) != 0 ? 1u : 0u;
+      want_prio = max(want_prio, lvl);
     }
     if (want_prio != prio_now) {
       if (want_prio == 3u) __builtin_amdgcn_s_setprio(3);
@@ -2559,16 +2597,17 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
 #ifdef RT_DBG_PX
       if (pxy == static_cast<uint32_t>(RT_DBG_PX))
         printf("dbgu s %d res %08x %08x %08x sum %08x %08x %08x\n", sample, __float_as_uint(res.x), __float_as_uint(res.y),
-               __float_as_uint(res.z), __float_as_uint(sum.x), __float_as_uint(sum.y), __float_as_uint(sum.z));
+               __float_as_uint(res.z), __float_as_uint(sum_get().x), __float_as_uint(sum_get().y), __float_as_uint(sum_get().z));
 #endif
-      sum = add(sum, res);
+      const f3 sum_now = add(sum_get(), res);
+      sum_put(sum_now);
       sample++;
       if (COUNT) c_samples++;
       if (probe) {
         probe_end = true;   // its rounds are added to the tile's cost at the top of the next round
         busy = false;
       } else if (sample == A.spp) {
-        const f3 c = mk(sum.x * A.sample_scale, sum.y * A.sample_scale, sum.z * A.sample_scale);
+        const f3 c = mk(sum_now.x * A.sample_scale, sum_now.y * A.sample_scale, sum_now.z * A.sample_scale);
         uint32_t *sq = nullptr;   // the staging slot of the pixel's tile, if the wave still holds it
         const uint32_t plr = pxy >> 16, pj = pxy & 0xffffu;
         if (n_stage != 0u) {

@@ -306,6 +306,7 @@ constexpr uint32_t kTailWord = 44;                   // work word of the tail pi
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)
+constexpr uint32_t kSumEntries = 6;        // u16 stack entries holding a lane's pixel sum (kParkSum traces)
 constexpr uint32_t kRcPoolChunksMax = 32;   // deep-level pool chunks per wave (one mask word)
 constexpr uint32_t kRcPoolHead = 17;         // per wave: the free-chunk mask word, then each lane's chunk byte (16 words)
 

@@ -698,9 +698,11 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   size_t rc_bytes = rc_levels * rc_level_bytes(4);
   // per-lane u16 stack: the reference walk's exact need, or the SAH walk's depth if deeper
   // (the mixed walk keeps a macro's SAH stack above the reference walk's entries)
+  // (+ kSumEntries on all-sphere worlds: the verified walk parks each lane's pixel sum in its stack's top entries)
   const uint32_t stack_cap = std::max({c->img.stack_need, c->accel_ok ? c->accel.depth + 1 : 0u,
                                        c->accel_w4 ? c->accel.wide_stack : 0u,
-                                       c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u});
+                                       c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u}) +
+                             (c->accel_ok ? rt::kSumEntries : 0u);
   // (+ the block's RNG slots, kRngSlotBytes: the "stack" region's fixed tail)
   const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2 + kRngSlotBytes;
   size_t stack_bytes = stackless ? kRngSlotBytes : full_stack_bytes;

@@ -451,16 +451,17 @@ bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std:
 // The verified sphere walk is latency-bound (dependent node loads): hipRTC allocates its render kernel
 // ~97 VGPRs (4 waves/SIMD); asked for 6 waves (80 VGPRs) it runs the 10k frame 226-231 -> 206-208 ms
 // (profiles/r03_ab_jit_waves.jsonl).  RT_ACCEL_WAVES=N overrides (0: the allocator's own choice);
-// RT_JIT_WAVES, when set, applies to every run-time kernel instead.  Every width is asked for 5 (round 5; rounds 3-4:
-// 6).  The 6-wave build (80 VGPRs) spills VGPRs, and twice a build of it rendered wrong pixels where the same source at
-// 5 waves or at the allocator's budget was exact: the 4-wide walk of round 4, and in round 5 the 2-wide walk once the
-// tail-piece hand-out was compiled in (G and B of samples in mixed waves, a fault at the full 10k config); with its
-// SGPR spills in scratch instead of VGPR lanes the same 6-wave build was exact.  At 5 waves the walk needs no VGPR
-// spill (87 VGPRs) and runs within noise of 6 (profiles/r05_ab_s21_10k.jsonl).
+// RT_JIT_WAVES, when set, applies to every run-time kernel instead.  Every width is asked for 6 waves (80 VGPRs), and the
+// build is kept only if it spills no VGPR (kAccelWavesScratchMax = 0; else the allocator's build and a spill-free raise):
+// twice a 6-wave build that spilled VGPRs rendered wrong pixels where the same source without VGPR spills was exact —
+// the 4-wide walk of round 4, and in round 5 the 2-wide walk once the tail-piece hand-out was compiled in (G and B of
+// samples in mixed waves, a fault at the full 10k config); with its SGPR spills in scratch the same build was exact.
+// Since round 5 the 2-wide walk reaches 80 VGPRs without spilling (the pixel sum parked in the lane's stack, the tail
+// priority by ballots, the root through a scalar operand).
 int accel_waves(int /*wide*/) {
   if (std::getenv("RT_JIT_WAVES")) return 0;
   if (const char *e = std::getenv("RT_ACCEL_WAVES")) return std::max(0, std::min(8, std::atoi(e)));
-  return 5;
+  return 6;
 }
 
 // Width of the verified sphere walk's tree: 2 (the SAH BVH2) or 4 (its 4-wide collapse, accel::collapse_wide)
@@ -476,7 +477,7 @@ bool accel_quant() {
   return false;
 }
 
-// The default request is measured on the plain 10k walk (87 VGPRs at 5 waves, no scratch).  Variants that need more
+// The default request is measured on the plain 10k walk (80 VGPRs at 6 waves, no scratch).  Variants that need more
 // registers (noise, image u,v, deep bounces: 125-149 VGPRs) would spill; a default-request build with any scratch is
 // replaced by the allocator's own build (+ the residency raise, itself spill-free).  An explicit RT_ACCEL_WAVES is kept
 // as built.
