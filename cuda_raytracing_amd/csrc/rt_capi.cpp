@@ -838,7 +838,16 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     const uint32_t per_word = 4u / cb;
     const size_t used = ((rc_levels + per_word - 1) / per_word * per_word) * rc_level_bytes(cb) + stack_bytes + kLdsReserve;
     const size_t node_bytes = static_cast<size_t>(node_words) * 4;
-    const size_t room = used < kLdsPerCu ? (kLdsPerCu - used) / node_bytes : 0;
+    size_t room = used < kLdsPerCu ? (kLdsPerCu - used) / node_bytes : 0;
+    // By default the colour stack comes first: staged nodes only take what a block at kRcLdsOnlyBlocks per CU leaves
+    // once every level fits beside the stacks (round 5: the 10k walk's parked pixel sum made the stacks 3 KB larger,
+    // and 64 staged nodes then left 8 of its 16 levels, whose HBM twins cost 1.6 GB per frame at the same speed:
+    // profiles/r05_ab_s37_10k.jsonl).  An explicit RT_ACCEL_LDS_NODES keeps the round-4 rule above.
+    if (!c->accel_lds_set && c->rc_lds_auto) {
+      const size_t all = static_cast<size_t>((mb + per_word - 1) / per_word * per_word) * rc_level_bytes(cb) + stack_bytes + kLdsReserve;
+      const size_t budget = kLdsPerCu / kRcLdsOnlyBlocks;
+      room = std::min(room, all < budget ? (budget - all) / node_bytes : 0);
+    }
     accel_lds_nodes = static_cast<uint32_t>(std::min<size_t>(accel_lds_nodes, room));
     scene_lds_words = accel_lds_nodes * node_words;
   }
