@@ -662,6 +662,28 @@ def test_full_size_config_rows_match_oracle(idx, W, H, spp, b, stride, force):
     assert bad.size == 0, f"{len(bad)} values differ, first at row {bad[0][0] * stride} col {bad[0][1]}"
 
 
+@pytest.mark.parametrize("idx,W,H,spp,b,rows", [
+    (0, 1920, 1080, 512, 16, 2),      # config 2
+    (1, 1920, 1080, 1024, 50, 1),     # config 3 (Cornell)
+    (17, 1920, 1080, 1024, 50, 2),    # config 3 (Perlin)
+    (20, 1920, 1080, 256, 16, 2),     # config 4
+    (0, 3840, 2160, 2048, 50, 1),     # config 5
+])
+def test_full_spp_config_rows_match_oracle(idx, W, H, spp, b, rows):
+    # every BASELINE config at its FULL sample count and depth: a shard of rows through the middle of the frame (the
+    # rows' own global pixel indices seed their RNG streams), rendered by the default policy, equals the oracle's
+    # rendering of the same rows bit for bit
+    w, s = rt.build_scene(idx)
+    cam, W2, H2 = rt.camera_from_settings(s, W, H)
+    assert (W2, H2) == (W, H)
+    p = rt.make_params(s, W, H, spp=spp, bounces=b, row_offset=H // 2, row_stride=37, row_count=rows)
+    fb, st = gpu(w.scene(), cam, p)
+    rc, ref, _ = oracle_render(w.scene(), cam, p)
+    assert rc == 0 and fb.shape == ref.shape == (rows, W, 3)
+    bad = np.argwhere(bits(fb) != bits(ref))
+    assert bad.size == 0, f"{len(bad)} values differ, first at {bad[0].tolist()}"
+
+
 def test_fold_violation_rerenders_exactly(monkeypatch):
     # force the folded kernel's ray-bound flag (RT_FOLD_CHECK_BOUND lowers its threshold): rt_render must
     # re-render unfolded BEFORE copying the frame out, stats or not, and the PPM bytes of the context path
