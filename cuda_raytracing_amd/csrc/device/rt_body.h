@@ -340,7 +340,12 @@ __device__ f3 texture_color(const Mem<LDS> &S, const RenderArgs &A, uint32_t ti,
         f3 q = p;
         // unrolled: the octaves' table reads are independent, so their LDS latencies overlap (a
         // path trapped between the noise spheres runs alone on its SIMD at the end of the frame)
-#pragma unroll
+#ifndef RT_NOISE_UNROLL
+#define RT_NOISE_UNROLL 7
+#endif
+#define RT_STR_(x) #x
+#define RT_UNROLL_(n) _Pragma(RT_STR_(unroll n))
+        RT_UNROLL_(RT_NOISE_UNROLL)
         for (int oct = 0; oct < 7; ++oct) {
           accum += weight * perlin_noise(S, tb, q);
           weight *= 0.5f;

@@ -354,7 +354,11 @@ std::string jit_mixed_source(const SceneImage &img, int variant, int waves) {
   const char *pe = std::getenv("RT_MIX_PAUSE");
   const bool pause = !(pe && pe[0] == '0');
   const std::string mt = "MixedTraceK<" + std::to_string(scene_kinds(img)) + "u, " + (pause ? "true" : "false") + ">";
-  std::string src = "#include \"rt_body.h\"\nnamespace rt {\n";
+  // the noise octaves one at a time (RT_NOISE_UNROLL, rt_body.h): the unrolled loop's overlapped table reads were the
+  // mixed walk's register peak (165 VGPRs, 2 waves; 147 rolled, 3 waves without spilling).  RT_MIX_NOISE_UNROLL (A/B)
+  int unroll = 1;
+  if (const char *e = std::getenv("RT_MIX_NOISE_UNROLL")) unroll = std::max(1, std::min(7, std::atoi(e)));
+  std::string src = "#define RT_NOISE_UNROLL " + std::to_string(unroll) + "\n#include \"rt_body.h\"\nnamespace rt {\n";
   src += "extern \"C\" __global__ __launch_bounds__(256)" + waves_attr_n(waves) + " void rt_mixed_render(RenderArgs A) {\n  render_body<" +
          std::to_string(v | kVarNoProbe) + ", " + mt + ">(A);\n}\n";
   src += "extern \"C\" __global__ __launch_bounds__(256) void rt_mixed_render_count(RenderArgs A) {\n  render_body<" +
