@@ -100,7 +100,7 @@ class Stats(C.Structure):
         ("accel_spheres", C.c_int32), ("accel_depth", C.c_int32),
         ("accel_fallbacks", C.c_uint32), ("jit_source", C.c_int32), ("jit_ms", C.c_double),
         ("rc_hbm_slots", C.c_uint64), ("rc_lds_levels", C.c_int32), ("mix_macros", C.c_int32),
-        ("mix_fallbacks", C.c_uint32), ("pad_", C.c_int32),
+        ("mix_fallbacks", C.c_uint32), ("tiled_out", C.c_int32),
         ("render_kernel_ms", C.c_double), ("gather_ms", C.c_double), ("devices", C.c_int32), ("rc_pool_chunks", C.c_int32),
     ]
 

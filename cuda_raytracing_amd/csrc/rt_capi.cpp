@@ -308,7 +308,8 @@ struct rt_context {
   uint32_t tile_shift = 3;         // (tile_shift_setting)
   int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
-  bool tiled_out = false;          // RT_TILED_OUT=1: the render writes the frame tile-major, untile_kernel the rows + bytes
+  int tiled_out = -1;              // 1: the render writes the frame tile-major, untile_kernel the rows + bytes; 0: row-major
+                                   // stores; -1 (default): tile-major unless the scene has noise textures (RT_TILED_OUT)
   bool used_tiled = false;         // the last render's
   int tail_chunk = 0;              // RT_TAIL_CHUNK: the tail of the order in pieces of this many pixels (0: whole tiles)
   double tail_gen = 1.0;           // RT_TAIL_GEN: ... over this many times the grid's lanes of ids
@@ -524,7 +525,7 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
     c->tail_chunk = (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32) ? v : 0;
   }
   if (const char *e = std::getenv("RT_TAIL_GEN")) c->tail_gen = std::max(0.0, std::atof(e));
-  if (const char *e = std::getenv("RT_TILED_OUT")) c->tiled_out = e[0] == '1';
+  if (const char *e = std::getenv("RT_TILED_OUT")) c->tiled_out = e[0] == '1' ? 1 : (e[0] == '0' ? 0 : -1);
   if (const char *e = std::getenv("RT_ACCEL_LDS_NODES")) {
     c->accel_lds_nodes = static_cast<uint32_t>(std::max(0, std::atoi(e)));
     c->accel_lds_set = true;
@@ -726,8 +727,11 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
   const bool rc_lds_only = c->rc_lds_auto && !c->rc_lds_only_off && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
-  // tile-major output (run-time kernels; not with output staging, which stores whole tiles row-major itself)
-  const bool tiled_kernel = c->tiled_out && c->stage_slots == 0 && out_dev != nullptr;
+  // tile-major output (run-time kernels; not with output staging, which stores whole tiles row-major itself).  By
+  // default not in kernels with noise textures: there the same store made the Perlin d50 kernel 15-21 % slower at the
+  // same registers and LDS (code generation; scene 0, Cornell and 10k within 0-1 %)
+  const bool tiled_kernel = (c->tiled_out == 1 || (c->tiled_out < 0 && !c->img.has_noise)) && c->stage_slots == 0 &&
+                            out_dev != nullptr;
   // the deep-level pool's code in run-time kernels with HBM levels (sized below, once the residency is known)
   // (by default deep kernels with automatic levels; pinned levels, RT_RC_LDS_LEVELS, get one only with RT_RC_POOL)
   const bool pool_kernel = c->rc_pool > 0 && !rc_lds_only &&
@@ -1257,6 +1261,7 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   if (!c->rendered) return RT_OK;
   st->rc_lds_levels = static_cast<int32_t>(c->used_rc_levels);
   st->rc_pool_chunks = static_cast<int32_t>(c->used_pool_chunks);
+  st->tiled_out = c->used_tiled ? 1 : 0;
   st->jit_source = c->jit_source;
   st->jit_ms = c->jit_ms;
   DeviceGuard g(c->device);
@@ -1420,8 +1425,11 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0) |
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0) |
                       static_cast<int>(tile_shift_setting() << rt::kVarTileShift) | (stage_slots_setting() ? rt::kVarStage : 0);
-  if (const char *e = std::getenv("RT_TILED_OUT"))
-    if (e[0] == '1' && !stage_slots_setting()) variant |= rt::kVarTiledOut;
+  {   // tile-major output as a render with a device frame decides (RT_TILED_OUT, noise textures, output staging)
+    const char *e = std::getenv("RT_TILED_OUT");
+    const int t = e ? (e[0] == '1' ? 1 : (e[0] == '0' ? 0 : -1)) : -1;
+    if ((t == 1 || (t < 0 && !img.has_noise)) && !stage_slots_setting()) variant |= rt::kVarTiledOut;
+  }
   {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks), else the pool's code
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);
     const size_t need = static_cast<size_t>((mb + 3) & ~3u) * rc_level_bytes(cb) +

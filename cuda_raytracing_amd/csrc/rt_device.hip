@@ -186,22 +186,27 @@ __global__ __launch_bounds__(256) void tonemap_kernel(const float *__restrict__ 
 }
 
 // Tile-major render output (kVarTiledOut) -> the row-major float frame and, fused, the PPM bytes of the same floats.
-// One thread per output float: the writes are contiguous, the reads gather 12-B pixels from 768-B tiles.
+// One block per band of one tile row x kUntileCols columns: its reads are whole tiles (one XCD's L2 fetches each tile
+// line once) and its writes whole 128-B lines of the float rows (kUntileCols x 12 B) and of the byte rows (x 3 B).
+constexpr uint32_t kUntileCols = 128;
 __global__ __launch_bounds__(256) void untile_kernel(const float *__restrict__ tiled, float *__restrict__ out,
                                                      uint8_t *__restrict__ out8, uint32_t rows, uint32_t width,
                                                      uint32_t tiles_x, uint32_t ts) {
-  const uint64_t e = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  if (e >= static_cast<uint64_t>(rows) * width * 3u) return;
-  const uint32_t p = static_cast<uint32_t>(e / 3u), c = static_cast<uint32_t>(e - 3ull * p);
-  const uint32_t lr = p / width, j = p - lr * width, tsh = 6u - ts;
-  const uint32_t tile = (lr >> tsh) * tiles_x + (j >> ts);
-  const uint32_t k = ((lr & ((1u << tsh) - 1u)) << ts) | (j & ((1u << ts) - 1u));
-  const float v = tiled[static_cast<size_t>(tile) * 192u + 3u * k + c];
-  out[e] = v;
-  if (out8) {
-    const float g = v > 0 ? sqrtf(v) : 0.0f;
-    const float q = (g < 0.0f) ? 0.0f : ((g > 0.999f) ? 0.999f : g);
-    out8[e] = static_cast<uint8_t>(static_cast<uint32_t>(256 * q) & 0xffu);
+  const uint32_t tsh = 6u - ts, th = 1u << tsh, x0 = blockIdx.x * kUntileCols, y0 = blockIdx.y * th;
+  for (uint32_t idx = threadIdx.x; idx < th * kUntileCols * 3u; idx += 256u) {
+    const uint32_t r = idx / (kUntileCols * 3u), f = idx - r * (kUntileCols * 3u);
+    const uint32_t j = f / 3u, c = f - 3u * j, x = x0 + j, y = y0 + r;
+    if (x >= width || y >= rows) continue;
+    const uint32_t tile = blockIdx.y * tiles_x + (x >> ts);
+    const uint32_t k = (r << ts) | (x & ((1u << ts) - 1u));
+    const float v = tiled[static_cast<size_t>(tile) * 192u + 3u * k + c];
+    const size_t e = (static_cast<size_t>(y) * width + x) * 3u + c;
+    out[e] = v;
+    if (out8) {
+      const float g = v > 0 ? sqrtf(v) : 0.0f;
+      const float q = (g < 0.0f) ? 0.0f : ((g > 0.999f) ? 0.999f : g);
+      out8[e] = static_cast<uint8_t>(static_cast<uint32_t>(256 * q) & 0xffu);
+    }
   }
 }
 
@@ -321,10 +326,10 @@ hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t 
 
 hipError_t launch_untile(const float *tiled, float *out, uint8_t *out8, uint32_t rows, uint32_t width, uint32_t tiles_x,
                          uint32_t ts, hipStream_t s) {
-  const uint64_t n = static_cast<uint64_t>(rows) * width * 3u;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(untile_kernel, dim3(static_cast<uint32_t>((n + 255) / 256)), dim3(256), 0, s, tiled, out, out8, rows,
-                     width, tiles_x, ts);
+  if (rows == 0 || width == 0 || ts > 6u) return rows == 0 || width == 0 ? hipSuccess : hipErrorInvalidValue;
+  const uint32_t th = 1u << (6u - ts);
+  hipLaunchKernelGGL(untile_kernel, dim3((width + kUntileCols - 1) / kUntileCols, (rows + th - 1) / th), dim3(256), 0, s,
+                     tiled, out, out8, rows, width, tiles_x, ts);
   return hipGetLastError();
 }
 

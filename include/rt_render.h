@@ -137,7 +137,8 @@ typedef struct rt_stats {
   int32_t rc_lds_levels;   /* colour-stack levels the last render kept in LDS (deeper ones live in HBM) */
   int32_t mix_macros;      /* RT_TRAV_MIXED: transform-free subtrees with a SAH walk (0 otherwise) */
   uint32_t mix_fallbacks;  /* RT_TRAV_MIXED: macro walks of the last render handed back to the reference walk */
-  int32_t pad_;
+  int32_t tiled_out;       /* 1: the last render wrote the float frame tile-major (coalesced 128-B lines) and a second
+                              kernel wrote the caller's row-major floats and bytes; 0: each pixel stored row-major */
   /* ABI 5 */
   double render_kernel_ms; /* the render kernel alone: its first wave's start to its last wave's end on the device's
                               wall clock (s_memrealtime), what a profiler reports as the kernel duration; render_ms

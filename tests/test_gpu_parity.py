@@ -491,15 +491,21 @@ def test_fused_ppm_bytes_match_host_tonemap(idx, W, H, spp, b):
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
 
 
+@pytest.mark.parametrize("tiled", ["1", "0", "auto"])
 @pytest.mark.parametrize("tile_w", ["8", "32"])
 @pytest.mark.parametrize("idx,W,H,spp,b", [(0, 96, 54, 8, 16), (17, 64, 36, 4, 50), (1, 40, 40, 4, 50), (20, 72, 44, 2, 8),
-                                           (3, 40, 40, 2, 8), (0, 33, 7, 2, 16)])
-def test_tiled_output_matches_oracle(idx, W, H, spp, b, tile_w, monkeypatch):
-    # RT_TILED_OUT: the render kernel writes the float frame tile-major and untile_kernel writes the caller's row-major
-    # floats and the P6 bytes — bit-identical to the oracle and to the host tonemap, partial edge tiles included, on
-    # the static (LDS-only and pooled deep kernels), verified sphere and mixed walks, 8x8 and 32x2 tiles
+                                           (3, 40, 40, 2, 8), (0, 33, 7, 2, 16), (0, 260, 20, 1, 4)])
+def test_tiled_output_matches_oracle(idx, W, H, spp, b, tile_w, tiled, monkeypatch):
+    # Tile-major output (the default without noise textures; RT_TILED_OUT=0: each pixel stored row-major with its bytes
+    # by the render kernel, =1: tile-major in every kernel):
+    # the render kernel writes the float frame tile-major and untile_kernel writes the caller's row-major floats and
+    # the P6 bytes in 128-column bands — bit-identical to the oracle and to the host tonemap, partial edge tiles and
+    # bands included, on the static (LDS-only and pooled deep kernels), verified sphere and mixed walks, 8x8 and 32x2
     import torch
-    monkeypatch.setenv("RT_TILED_OUT", "1")
+    if tiled == "auto":
+        monkeypatch.delenv("RT_TILED_OUT", raising=False)
+    else:
+        monkeypatch.setenv("RT_TILED_OUT", tiled)
     monkeypatch.setenv("RT_TILE_W", tile_w)
     w, s = rt.build_scene(idx)
     cam, W, H = rt.camera_from_settings(s, W, H)
@@ -513,8 +519,10 @@ def test_tiled_output_matches_oracle(idx, W, H, spp, b, tile_w, monkeypatch):
     rc, ref, _ = oracle_render(w.scene(), cam, p)
     assert rc == 0 and np.array_equal(bits(fb), bits(ref))
     assert np.array_equal(out8.cpu().numpy(), rt.tonemap(ref))
-    fb2, _ = gpu(w.scene(), cam, p)   # the one-shot entry point (host copy of the floats)
+    fb2, st = gpu(w.scene(), cam, p)   # the one-shot entry point (host copy of the floats)
     assert np.array_equal(bits(fb2), bits(ref))
+    noise = idx in (3, 17)   # final_scene's marble sphere, perlin_spheres
+    assert st.tiled_out == (1 if tiled == "1" or (tiled == "auto" and not noise) else 0)
 
 
 def _random_world(seed: int):
