@@ -993,21 +993,22 @@ struct AccelTraceK {
         if (n <= cap) {
           walking = false;
           const float dl = sqrtf(dot(r.d, r.d));
-          const uint32_t q = A.prim_words >> 2;   // uint4 per entry
           const float rho = A.prim_rho;
-          const uint4 *L = reinterpret_cast<const uint4 *>(A.prim_lists) + static_cast<size_t>(tile) * cap * q;
-          // entry k's words loaded one iteration ahead (its loads under entry k-1's test)
-          uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
-          if (n > 0) { e0 = L[0]; e1 = L[1]; }
+          // 8-B entries (SAH prim index, axial bound); the sphere's centre, motion and r^2 from the tree's prims (the
+          // walk's own leaf words, L2-resident): entry k+1 is loaded under entry k's test (32-B entries with the
+          // sphere inline evicted the frame's lines from L2 before their tiles had filled them: twice the memory
+          // writes)
+          const uint2 *L = reinterpret_cast<const uint2 *>(A.prim_lists) + static_cast<size_t>(tile) * cap;
+          uint2 c1 = n > 0 ? L[0] : make_uint2(0, 0);
           for (uint32_t k = 0; k < n; ++k) {
-            const uint4 a0 = e0, a1 = e1;
-            const uint32_t e2z = q > 2 ? L[k * q + 2].x : 0u;
-            if (k + 1 < n) { e0 = L[(k + 1) * q]; e1 = L[(k + 1) * q + 1]; }
-            if (__uint_as_float(a1.y) > __builtin_fmaf(T.tmax, dl, rho) * 1.0000010f) break;
+            const uint2 c = c1;
+            if (__uint_as_float(c.y) > __builtin_fmaf(T.tmax, dl, rho) * 1.0000010f) break;
+            const uint4 a0 = P[c.x * 4], a1 = P[c.x * 4 + 1];
+            if (k + 1 < n) c1 = L[k + 1];
             if (COUNT) vc.xp++;
             if (sphere_hit_tie<UV, true, false>(T, r, h, 0u, mk(asf(a0.x), asf(a0.y), asf(a0.z)),
-                                                mk(asf(a1.z), asf(a1.w), asf(e2z)), asf(a0.w), 0.0f, sa2, sra2, tie))
-              best = a1.x;
+                                                mk(asf(a0.w), asf(a1.x), asf(a1.y)), asf(a1.z), 0.0f, sa2, sra2, tie))
+              best = c.x;
           }
         }
       }

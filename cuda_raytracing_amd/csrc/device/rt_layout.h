@@ -52,7 +52,7 @@ constexpr int kAccel4QNodeWords = 16, kAccel4QRef = 10;
 // Primary-ray candidate list entry (prim_list_kernel): the sphere inline, so a camera ray's list loop loads one
 // entry per sphere: words 0..3 = centre at time 0 and r^2, 4 = SAH prim index, 5 = axial lower bound (float bits),
 // 6..7 = motion x, y, 8 = motion z (entries of 12 words when some sphere moves, else 8 and no motion)
-enum : int { kPrimEntryIdx = 4, kPrimEntryBound = 5, kPrimEntryMotion = 6 };
+enum : int { kPrimEntryIdx = 0, kPrimEntryBound = 1, kPrimEntryWords = 2 };   // sphere index, axial bound
 constexpr uint32_t kAccelLeaf = 0x80000000u;
 constexpr float kAccelKappa = 1.953125e-3f;   // 2^-9 >= sqrt(32 * 2^-24): cone padding per unit of |oc|
 enum : int { AP_CENTER = 0, AP_MOTION = 3, AP_RADIUS2 = 6, AP_INV_RADIUS = 7, AP_MAT = 8, AP_NODE = 9, AP_VBOX = 10 };
@@ -257,10 +257,11 @@ struct RenderArgs {
   // Primary-ray candidate lists (verified sphere walk; prim_list_kernel): per 8x8 tile of the shard, the spheres
   // whose padded ball meets the cone that holds every camera ray of the tile, ascending by a lower bound of
   // their distance along the cone axis; a camera ray tests them in that order instead of walking the tree
-  const uint32_t *prim_lists;     // [tiles][prim_cap] entries of prim_words words (kPrimEntry*); null = off
+  const uint32_t *prim_lists;     // [tiles][prim_cap] entries of prim_words words (kPrimEntry*: SAH prim index and
+                                  // axial bound; the sphere's words are read from the tree's prims); null = off
   const uint32_t *prim_counts;    // [tiles] entries; > prim_cap: no list (overflow), the ray walks the tree
   uint32_t prim_cap;
-  uint32_t prim_words;            // 8, or 12 when some sphere moves (the motion words)
+  uint32_t prim_words;            // kPrimEntryWords
   float prim_rho;                 // bound on |ray origin - camera centre| (defocus disc, rounding included)
   uint32_t defer_trace;           // verified traversal: the round's walk stops once at most this many
   uint32_t trace_min_iters;       // lanes (and <= 1/4 of the starters) still walk, after this many steps

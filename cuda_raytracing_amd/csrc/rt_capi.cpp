@@ -1113,7 +1113,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
     // primary-ray candidate lists of this frame's camera (device/prim_lists.h), before the probe and the render
     float prim_rho = 0.0f;
     const rt::PrimListGeom g = make_prim_geom(cam, p, tiles_x, tile_shift, c->accel_half_motion, &prim_rho);
-    const uint32_t words = c->accel_half_motion > 0 ? 12u : 8u;
+    const uint32_t words = rt::kPrimEntryWords;
     if (c->prim_lists.ensure(static_cast<size_t>(n_tiles) * c->prim_cap * words * 4) != hipSuccess ||
         c->prim_counts.ensure(static_cast<size_t>(n_tiles) * 4) != hipSuccess)
       return RT_ERR_HIP;

@@ -290,13 +290,10 @@ __global__ __launch_bounds__(64) void prim_list_kernel(PrimListGeom g, const uin
     const uint2 e = cand[i];
     uint32_t rank = 0;
     for (uint32_t j = 0; j < n; ++j) rank += prim_before(cand[j], e) ? 1u : 0u;
-    // the entry with the sphere inline (rt_layout.h kPrimEntry*)
-    const uint32_t *pw = prims + static_cast<size_t>(e.x) * kAccelPrimWords;
+    // the entry: the sphere's SAH prim index and its axial bound (rt_layout.h kPrimEntry*)
     uint32_t *o = out + static_cast<size_t>(rank) * words;
-    o[0] = pw[AP_CENTER]; o[1] = pw[AP_CENTER + 1]; o[2] = pw[AP_CENTER + 2]; o[3] = pw[AP_RADIUS2];
-    o[kPrimEntryIdx] = e.x; o[kPrimEntryBound] = e.y;
-    o[kPrimEntryMotion] = pw[AP_MOTION]; o[kPrimEntryMotion + 1] = pw[AP_MOTION + 1];
-    if (words > 8) { o[8] = pw[AP_MOTION + 2]; o[9] = 0; o[10] = 0; o[11] = 0; }
+    o[kPrimEntryIdx] = e.x;
+    o[kPrimEntryBound] = e.y;
   }
   if (lane == 0) counts[tile] = n;
 }
@@ -307,7 +304,7 @@ hipError_t launch_prim_lists(const PrimListGeom &g, const uint32_t *nodes, uint3
                              uint32_t n_tiles, uint32_t cap, uint32_t words, uint32_t *lists, uint32_t *counts,
                              hipStream_t s) {
   if (n_tiles == 0) return hipSuccess;
-  if (cap == 0 || cap > kPrimMaxCap || (words != 8 && words != 12)) return hipErrorInvalidValue;
+  if (cap == 0 || cap > kPrimMaxCap || words != static_cast<uint32_t>(kPrimEntryWords)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(prim_list_kernel, dim3(n_tiles), dim3(64), 0, s, g, nodes, root, prims, n_tiles, cap, words, lists,
                      counts);
   return hipGetLastError();

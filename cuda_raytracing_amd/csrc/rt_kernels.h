@@ -24,7 +24,7 @@ hipError_t launch_untile(const float *tiled, float *out, uint8_t *out8, uint32_t
 hipError_t launch_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t tiles_x, hipStream_t s);
 hipError_t launch_render(const RenderArgs &a, int variant, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 // primary-ray candidate lists of the verified sphere walk, one per 8x8 tile of the shard (device/prim_lists.h)
-// (entries of `words` words with the sphere inline, rt_layout.h kPrimEntry*)
+// (entries of `words` = kPrimEntryWords words: SAH prim index and axial bound, rt_layout.h kPrimEntry*)
 hipError_t launch_prim_lists(const PrimListGeom &g, const uint32_t *nodes, uint32_t root, const uint32_t *prims,
                              uint32_t n_tiles, uint32_t cap, uint32_t words, uint32_t *lists, uint32_t *counts,
                              hipStream_t s);
