@@ -55,6 +55,9 @@ std::vector<std::string> jit_extra_options() {
   // RT_JIT_SGPR_MEM=1 (A/B): scalar-register spills go to scratch memory instead of lanes of spill VGPRs
   if (const char *e = std::getenv("RT_JIT_SGPR_MEM"))
     if (e[0] == '1') { v.push_back("-mllvm"); v.push_back("-amdgpu-spill-sgpr-to-vgpr=0"); }
+  // RT_JIT_SCHED=<strategy> (A/B): the machine scheduler's strategy (max-ilp, max-memory-clause, iterative-ilp, ...)
+  if (const char *e = std::getenv("RT_JIT_SCHED"))
+    if (e[0] != '\0') { v.push_back("-mllvm"); v.push_back(std::string("-amdgpu-sched-strategy=") + e); }
   if (const char *e = std::getenv("RT_JIT_OPTS")) {
     std::string cur;
     for (const char *p = e;; ++p) {
@@ -102,14 +105,16 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
 // 86 -> 71 VGPRs on scene 0; measured again in round 1: +30 % frame time).  RT_JIT_OPTS appends options
 // (A/B experiments); hipRTC keeps the FIRST of two conflicting flags, so it cannot override these.
 // The on-disk cache key hashes this whole vector (build_module): bit-exact parity rests on these flags.
-std::vector<std::string> jit_options(const std::string &arch) {
+std::vector<std::string> jit_options(const std::string &arch, const std::vector<std::string> &extra) {
   std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
   for (const std::string &x : jit_extra_options()) o.push_back(x);
+  for (const std::string &x : extra) o.push_back(x);
   return o;
 }
 
-bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log) {
+bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log,
+                 const std::vector<std::string> &extra) {
   hiprtcProgram prog;
   const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
   const char *hdr_names[] = {"rt_layout.h", "rt_body.h"};
@@ -117,7 +122,7 @@ bool jit_compile(const std::string &src, const std::string &arch, std::vector<ch
     if (log) *log = "hiprtcCreateProgram failed";
     return false;
   }
-  const std::vector<std::string> o = jit_options(arch);
+  const std::vector<std::string> o = jit_options(arch, extra);
   std::vector<const char *> opts;
   for (const std::string &x : o) opts.push_back(x.c_str());
   const hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(opts.size()), opts.data());
@@ -229,13 +234,14 @@ std::string toolchain_tag() {
 }
 
 // Compile (or fetch) the module of `src` exporting <prefix>_render, <prefix>_render_count, <prefix>_probe.
-bool build_module(const std::string &src, const std::string &prefix, JitKernels *out, std::string *why) {
+bool build_module(const std::string &src, const std::string &prefix, JitKernels *out, std::string *why,
+                  const std::vector<std::string> &extra = {}) {
   const auto t0 = std::chrono::steady_clock::now();
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) dev = 0;
   const std::string arch = arch_of(dev);
   std::string opts;
-  for (const std::string &x : jit_options(arch)) opts += x + " ";
+  for (const std::string &x : jit_options(arch, extra)) opts += x + " ";
   const std::string disk_key = arch + "|" + toolchain_tag() + "|" + opts + "|" + src;
   const std::string key = std::to_string(dev) + "|" + disk_key;
   std::lock_guard<std::mutex> lock(g_mu);
@@ -251,7 +257,7 @@ bool build_module(const std::string &src, const std::string &prefix, JitKernels 
     const std::string path = dir.empty() ? "" : dir + name;
     bool have = !path.empty() && disk_load(path, disk_key, &code);
     source = have ? RT_JIT_DISK : RT_JIT_COMPILED;
-    if (!have && jit_compile(src, arch, &code, &log)) {
+    if (!have && jit_compile(src, arch, &code, &log, extra)) {
       have = true;
       if (!path.empty()) disk_store(dir, path, disk_key, code);
     }
@@ -397,7 +403,7 @@ int render_vgprs(hipFunction_t fn, int *scratch) {
 
 // source(n): the module's source with the render kernel's attribute waves_attr_n(n) (n < 0: a cap of -n VGPRs)
 template <class Source>
-void raise_residency(const Source &source, const char *prefix, JitKernels *out) {
+void raise_residency(const Source &source, const char *prefix, JitKernels *out, const std::vector<std::string> &extra = {}) {
   if (std::getenv("RT_JIT_WAVES") || std::getenv("RT_JIT_MAX_VGPR")) return;
   if (const char *e = std::getenv("RT_JIT_RAISE")) if (e[0] == '0') return;
   int sc0 = 0;
@@ -409,7 +415,7 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out) 
   if (v0 - limit > kRaiseSlack) return;
   JitKernels k = *out;
   std::string why;
-  if (!build_module(source(-limit), prefix, &k, &why)) return;
+  if (!build_module(source(-limit), prefix, &k, &why, extra)) return;
   int sc = 0;
   const int v = render_vgprs(k.render, &sc);
   if (std::getenv("RT_DEBUG"))
@@ -487,11 +493,23 @@ bool accel_quant() {
 // as built.
 constexpr int kAccelWavesScratchMax = 0;   // round 4: 96 B (see accel_waves)
 
+// The verified sphere walk's machine-scheduler strategy: max-ilp (the walk's dependent node loads and slab tests
+// scheduled for instruction-level parallelism).  Same box (profiles/r05_ab_s54_*): 10k 193.7 / 193.2 ms vs 210.8 /
+// 220.1 with the default strategy, at the same 80 VGPRs without a spill; the static kernels keep the default (Perlin
+// +23 % under max-ilp, scene 0 level).  RT_ACCEL_SCHED=<strategy> overrides, RT_ACCEL_SCHED=0 keeps the default.
+std::vector<std::string> accel_sched() {
+  std::string s = "max-ilp";
+  if (const char *e = std::getenv("RT_ACCEL_SCHED")) s = e;
+  if (s.empty() || s == "0" || s == "default") return {};
+  return {"-mllvm", "-amdgpu-sched-strategy=" + s};
+}
+
 bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
   int w = accel_waves(wide);
-  if (!build_module(jit_accel_source(img, variant, w, wide), "rt_accel", out, why)) return false;
+  const std::vector<std::string> sched = accel_sched();
+  if (!build_module(jit_accel_source(img, variant, w, wide), "rt_accel", out, why, sched)) return false;
   if (w > 0 && !std::getenv("RT_ACCEL_WAVES")) {
     int sc = 0;
     render_vgprs(out->render, &sc);
@@ -499,13 +517,13 @@ bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels 
       std::fprintf(stderr, "[rt] jit accel waves_per_eu(%d): scratch %d B per lane\n", w, sc);
     if (sc < 0 || sc > kAccelWavesScratchMax) {
       JitKernels k = *out;
-      if (!build_module(jit_accel_source(img, variant, 0, wide), "rt_accel", &k, why)) return false;
+      if (!build_module(jit_accel_source(img, variant, 0, wide), "rt_accel", &k, why, sched)) return false;
       k.ms += out->ms;
       *out = k;
       w = 0;
     }
   }
-  if (w == 0) raise_residency([&](int n) { return jit_accel_source(img, variant, n, wide); }, "rt_accel", out);
+  if (w == 0) raise_residency([&](int n) { return jit_accel_source(img, variant, n, wide); }, "rt_accel", out, sched);
   return true;
 }
 

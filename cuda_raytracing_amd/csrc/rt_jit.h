@@ -29,7 +29,9 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
 bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fold, std::string *src, uint32_t *visits,
                 bool *folded = nullptr, int waves = 0);   // waves > 0: amdgpu_waves_per_eu (0: RT_JIT_WAVES or none)
 // Compile `src` for `arch` (e.g. "gfx950"); on success the code object is in *code.  No device needed.
-bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log);
+// `extra`: options after the common ones (the verified sphere walk's scheduler strategy, accel_sched)
+bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log,
+                 const std::vector<std::string> &extra = {});
 
 // Per-lane DFS kernels specialised on the node kinds present in the scene (large scenes: the
 // kind dispatch of trav_step keeps only those branches).  Same contract as jit_kernels.
@@ -52,7 +54,7 @@ int scene_shading_bits(const SceneImage &img);
 // extra hipRTC options from the RT_JIT_OPTS environment variable (space separated)
 std::vector<std::string> jit_extra_options();
 // the complete hipRTC option vector for `arch` (numerics flags + RT_JIT_OPTS); hashed into the disk-cache key
-std::vector<std::string> jit_options(const std::string &arch);
+std::vector<std::string> jit_options(const std::string &arch, const std::vector<std::string> &extra = {});
 
 hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes);
