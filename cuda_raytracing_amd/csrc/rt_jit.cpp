@@ -427,6 +427,20 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out, 
   }
 }
 
+// Machine-scheduler strategy options: "-amdgpu-sched-strategy=max-ilp" when `on`, unless the environment variable `env`
+// names another strategy (or 0 / default: the compiler's default strategy)
+std::vector<std::string> sched_options(const char *env, bool on) {
+  std::string s = on ? "max-ilp" : "";
+  if (const char *e = std::getenv(env)) s = e;
+  if (s.empty() || s == "0" || s == "default") return {};
+  return {"-mllvm", "-amdgpu-sched-strategy=" + s};
+}
+
+// The scene-specialised kernels keep the default strategy: under max-ilp scene 0 and 4K ran level, Cornell -5 % on one
+// box and level on another, Perlin +23 % (profiles/r05_ab_s54_*, r05_ab_s56_*, r05_ab_s57_*).  RT_STATIC_SCHED=<strategy>
+// (A/B) builds them with another.
+std::vector<std::string> static_sched(const SceneImage &) { return sched_options("RT_STATIC_SCHED", false); }
+
 bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
   std::string src;
   uint32_t visits = 0;
@@ -437,16 +451,17 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
   }
   out->visits = visits;
   out->folded = folded;
-  if (!build_module(src, "rt_static", out, why)) return false;
-  // one residency step up when the allocator lands just above a boundary (kept with at most kRaiseScratch bytes of
-  // scratch per lane: a spilled build is exact like any other — the round-4 6-wave mismatch was a lane-mask bool, §2)
+  const std::vector<std::string> sched = static_sched(img);
+  if (!build_module(src, "rt_static", out, why, sched)) return false;
+  // one residency step up when the allocator lands just above a boundary (kept only with at most raise_scratch()
+  // bytes of scratch per lane: none by default)
   raise_residency([&](int w) {
     std::string s2;
     uint32_t v2 = 0;
     bool f2 = false;
     jit_source(img, variant, max_visits, fold, &s2, &v2, &f2, w);
     return s2;
-  }, "rt_static", out);
+  }, "rt_static", out, sched);
   return true;
 }
 
@@ -497,12 +512,7 @@ constexpr int kAccelWavesScratchMax = 0;   // round 4: 96 B (see accel_waves)
 // scheduled for instruction-level parallelism).  Same box (profiles/r05_ab_s54_*): 10k 193.7 / 193.2 ms vs 210.8 /
 // 220.1 with the default strategy, at the same 80 VGPRs without a spill; the static kernels keep the default (Perlin
 // +23 % under max-ilp, scene 0 level).  RT_ACCEL_SCHED=<strategy> overrides, RT_ACCEL_SCHED=0 keeps the default.
-std::vector<std::string> accel_sched() {
-  std::string s = "max-ilp";
-  if (const char *e = std::getenv("RT_ACCEL_SCHED")) s = e;
-  if (s.empty() || s == "0" || s == "default") return {};
-  return {"-mllvm", "-amdgpu-sched-strategy=" + s};
-}
+std::vector<std::string> accel_sched() { return sched_options("RT_ACCEL_SCHED", true); }
 
 bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why) {
   out->visits = 0;
