@@ -26,7 +26,7 @@ HOST_SRC := $(CSRC)/host/rt_host.cpp $(CSRC)/host/image_load.cpp $(CSRC)/host/im
             $(CSRC)/host/image_png.cpp
 HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp $(CSRC)/xorwow_jump.cpp \
             $(CSRC)/sphere_accel.cpp $(CSRC)/mixed_accel.cpp \
-            $(CSRC)/scene_codegen.cpp $(CSRC)/rt_jit.cpp $(CSRC)/rt_multi.cpp
+            $(CSRC)/scene_codegen.cpp $(CSRC)/rt_jit.cpp $(CSRC)/rt_multi.cpp $(CSRC)/code_object.cpp
 HIP_HDR  := $(wildcard $(CSRC)/*.h) $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h \
             $(CSRC)/device/embedded_headers.inc include/rt_render.h include/rt_ref_layout.h
 

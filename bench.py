@@ -292,17 +292,62 @@ def launch_plan(gpus: int, env, device_count: int, backend: str = "nccl"):
     return "run", None
 
 
-def spawn_ranks(n: int, argv) -> int:
+def spawn_ranks(n: int, argv, script=None, env=None) -> int:
     """--gpus N without a launcher: run this script as N ranks under torch.distributed.run (one process per GPU,
-    rendezvous on 127.0.0.1), as a child process; returns its exit code.  This process has not touched the GPU."""
+    rendezvous on 127.0.0.1), as a child process; returns its exit code.  This process has not touched the GPU.
+    (script: another rank program under the same launcher — tests/dist_rank.py drives the gather path on CPU.)"""
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(script or Path(__file__).resolve()), *argv]
     log("launching: " + " ".join(cmd))
-    return subprocess.run(cmd).returncode
+    return subprocess.run(cmd, env=env).returncode
+
+
+def gather_frame(local_u8: "torch.Tensor", H: int, W: int, rank: int, world: int, backend: str):
+    """The frame's one collective: every rank's u8 PPM rows to rank 0 (RCCL over xGMI with "nccl"; host tensors with
+    gloo), re-interleaved there (multi_gpu.gather_rows); None on the other ranks."""
+    return gather_rows(local_u8 if backend == "nccl" else local_u8.cpu(), H, W, rank, world)
+
+
+def gather_check_step(H: int, world: int) -> int:
+    """Row stride of rank 0's check of the gathered frame: co-prime with the world size, so every rank's rows are among
+    the checked ones, and ~17 rows at 1080p (a bounded oracle sample); small frames: about 5 rows or more."""
+    step = 67 if H > 67 * 4 else max(1, H // 5)
+    while math.gcd(step, world) != 1:
+        step -= 1
+    return max(step, 1)
+
+
+def gather_check(img, H: int, W: int, world: int, reference_rows) -> dict:
+    """Rank 0, untimed: rows 0::step of the assembled frame against reference_rows(step) (u8 [rows, W, 3], the CPU
+    oracle's bytes of those rows — the checker).  The RNG subsequence is the global pixel index, so shards + gather +
+    un-permute must reproduce the oracle's rows byte for byte."""
+    import numpy as np
+    step = gather_check_step(H, world)
+    ref = np.asarray(reference_rows(step))
+    got = img[0::step].cpu().numpy()
+    return {"gather_bit_exact": bool(got.shape == ref.shape and np.array_equal(got, ref)),
+            "checked_rows": f"0::{step} ({ref.shape[0]} rows x {W} px, ranks {sorted({r % world for r in range(0, H, step)})})",
+            "checked_against": "CPU oracle (oracle/oracle_rt.c, the checker) bytes of those rows"}
+
+
+def oracle_rows_u8(world_, settings, cam, W, H, spp, bounces, step):
+    """The checker's bytes of rows 0::step: the CPU oracle's float rows (all host threads) through the host tonemap
+    (pixels_to_ppm's conversion, rt_host)."""
+    import ctypes as C
+    import numpy as np
+    rows = len(range(0, H, step))
+    p = rt.make_params(settings, W, H, spp=spp, bounces=bounces, row_offset=0, row_stride=step, row_count=rows)
+    out = np.zeros((rows, W, 3), np.float32)
+    st = _abi.Stats()
+    rc = _abi.oracle_lib().rt_render_cpu(C.byref(world_.scene()), C.byref(cam), C.byref(p),
+                                         out.ctypes.data_as(C.c_void_p), C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle rows failed: {rc}")
+    return rt.tonemap(out)
 
 
 def main():
@@ -391,10 +436,7 @@ def main():
         st = ctxs[i].timing()                                  # waits on that frame's render events
         torch.cuda.current_stream().wait_stream(s)
         if world_size > 1:
-            if args.dist_backend == "nccl":
-                img = gather_rows(outs8[i], H, W, rank, world_size)  # u8 rows: 3 B/pixel over xGMI
-            else:
-                img = gather_rows(outs8[i].cpu(), H, W, rank, world_size)
+            img = gather_frame(outs8[i], H, W, rank, world_size, args.dist_backend)   # u8 rows: 3 B/pixel over xGMI
             if img is not None:
                 gathered["img"] = img
         stats.append(st)
@@ -441,7 +483,9 @@ def main():
     spans = [st.render_kernel_ms if st.render_kernel_ms > 0 else st.render_ms for st in fstats]
     render_mean_ms = sum(spans) / len(spans)
     step_mean_ms = elapsed / args.steps * 1e3
-    assert render_mean_ms <= step_mean_ms, f"mean render span {render_mean_ms:.3f} ms > mean step {step_mean_ms:.3f} ms"
+    timing_consistent = render_mean_ms <= step_mean_ms
+    if not timing_consistent:
+        log(f"bench.py: timing defect: mean render span {render_mean_ms:.3f} ms > mean step {step_mean_ms:.3f} ms")
     seed_ms = med([st.init_ms for st in fstats])
     sched_ms = med([st.sched_ms for st in fstats])
     achieved = ops_per_sample * local_samples / (render_ms / 1e3) / 1e12
@@ -457,26 +501,18 @@ def main():
                      "frames_in_flight": 2, "steps": psteps, "ms_per_step": round(pel / psteps * 1e3, 3),
                      "render_ms_mean": round(sum(st.render_ms for st in pst) / len(pst), 3)}
 
-    # ---- N>1: rank 0 checks the gathered frame (untimed).  The RNG subsequence is the global pixel index, so
-    # its own render of a strided row sample (rows of every rank) must equal those rows of the assembled frame
-    # byte for byte: proof that the shards, the gather and the un-permute put every pixel in place ----
+    # ---- N>1: rank 0 checks the gathered frame (untimed) against the CPU oracle's bytes of a strided row sample
+    # (rows of every rank): the RNG subsequence is the global pixel index, so the shards, the gather and the
+    # un-permute must put every pixel in place byte for byte (the oracle is the checker here, never measured) ----
     dist_check = None
     if world_size > 1:
         dist_check = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
                       "gather_bytes_per_frame": max_shard_rows(H, world_size) * W * 3 * world_size,
                       "gather_bit_exact": None}
         if rank == 0 and "img" in gathered:
-            step = 67 if H > 67 * 4 else max(1, H // 5)   # co-prime with small world sizes: every rank's rows
-            rows_chk = len(range(0, H, step))
-            pchk = rt.make_params(settings, W, H, spp=args.spp, bounces=args.bounces, row_offset=0, row_stride=step,
-                                  row_count=rows_chk)
-            f32 = torch.empty((rows_chk, W, 3), dtype=torch.float32, device="cuda")
-            u8 = torch.empty((rows_chk, W, 3), dtype=torch.uint8, device="cuda")
-            ctx.render_into(cam, pchk, f32.data_ptr(), torch.cuda.current_stream().cuda_stream, u8.data_ptr())
-            ctx.timing()
-            got = gathered["img"][0::step].cpu()
-            dist_check["gather_bit_exact"] = bool(torch.equal(got, u8.cpu()))
-            dist_check["checked_rows"] = f"0::{step} ({rows_chk} rows x {W} px, ranks {sorted({r % world_size for r in range(0, H, step)})})"
+            dist_check.update(gather_check(gathered["img"], H, W, world_size,
+                                           lambda step: oracle_rows_u8(world, settings, cam, W, H, args.spp,
+                                                                       args.bounces, step)))
         dist.barrier()
 
     if rank == 0:
@@ -508,6 +544,7 @@ def main():
                            rt.RT_TRAV_MIXED: "rt_mixed_render (hipRTC)"}.get(
                     cst.traversal, "rt_lane_render (hipRTC)"),
             },
+            "timing_consistent": timing_consistent,
             "kernel_ms": {"render_median": round(render_ms, 3), "render_mean": round(render_mean_ms, 3),
                           "render_event_median": round(render_event_ms, 3),
                           "seed_median": round(seed_ms, 3),
@@ -552,6 +589,8 @@ def main():
         c.close()
     if world_size > 1:
         dist.destroy_process_group()
+    if not timing_consistent:   # the line above carries the measurement; the run still fails
+        sys.exit(3)
 
 
 if __name__ == "__main__":

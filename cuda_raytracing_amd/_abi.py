@@ -89,6 +89,21 @@ class Params(C.Structure):
     ]
 
 
+class KernelInfo(C.Structure):
+    """rt_kernel_info (ABI 6): a render kernel as the register allocator built it."""
+    _fields_ = [
+        ("vgprs", C.c_int32), ("agprs", C.c_int32), ("sgprs", C.c_int32), ("scratch_bytes", C.c_int32),
+        ("vgpr_spills", C.c_int32), ("sgpr_spills", C.c_int32), ("blocks_per_cu", C.c_int32), ("run_time", C.c_int32),
+        ("compiler", C.c_char * 128), ("loader", C.c_char * 128),
+    ]
+
+    def as_dict(self):
+        return {"vgprs": self.vgprs, "agprs": self.agprs, "sgprs": self.sgprs, "scratch_bytes": self.scratch_bytes,
+                "vgpr_spills": self.vgpr_spills, "sgpr_spills": self.sgpr_spills, "blocks_per_cu": self.blocks_per_cu,
+                "run_time": self.run_time, "compiler": self.compiler.decode(errors="replace"),
+                "loader": self.loader.decode(errors="replace")}
+
+
 class Stats(C.Structure):
     _fields_ = [
         ("init_ms", C.c_double), ("render_ms", C.c_double), ("total_ms", C.c_double),
@@ -102,6 +117,7 @@ class Stats(C.Structure):
         ("rc_hbm_slots", C.c_uint64), ("rc_lds_levels", C.c_int32), ("mix_macros", C.c_int32),
         ("mix_fallbacks", C.c_uint32), ("tiled_out", C.c_int32),
         ("render_kernel_ms", C.c_double), ("gather_ms", C.c_double), ("devices", C.c_int32), ("rc_pool_chunks", C.c_int32),
+        ("kernel", KernelInfo),
     ]
 
     def counter_dict(self):
@@ -179,7 +195,7 @@ HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_contex
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
                "rt_seed_states", "rt_kernel_source", "rt_mixed_build", "rt_multi_create", "rt_multi_render",
                "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map", "rt_accel_build_wide", "rt_rng_table_states",
-               "rt_accel_build_quant", "rt_prim_lists", "rt_multi_unpermute"]
+               "rt_accel_build_quant", "rt_prim_lists", "rt_multi_unpermute", "rt_kernel_build"]
 
 
 def _bind_single_hip_runtime():
@@ -236,6 +252,7 @@ def hip_lib():
         opt("rt_rng_table_states", C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_seed_states, C.c_int, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_int, P)
         _sig(L.rt_kernel_source, C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.c_char_p, C.c_uint64)
+        opt("rt_kernel_build", C.c_int, C.POINTER(Scene), C.c_int, C.c_int32, C.POINTER(KernelInfo))
         opt("rt_multi_create", C.c_int, C.POINTER(Scene), C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p))
         opt("rt_multi_render", C.c_int, P, C.POINTER(Camera), C.POINTER(Params), P, P, C.POINTER(Stats))
         opt("rt_multi_destroy", None, P)

@@ -2698,7 +2698,8 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     for (int off = 32; off > 0; off >>= 1) ms = max(ms, static_cast<uint32_t>(__shfl_xor(ms, off)));
     if (lane == 0) {
       atomicMax(&A.counters[CNT_MAX_STACK], static_cast<unsigned long long>(ms));
-      if (ms > A.stack_cap) atomicAdd(&A.counters[CNT_OVERFLOW], 1ull);
+      // (kParkSum traces: the top kSumEntries entries hold the pixel sum, so the walk's own capacity is below them)
+      if (ms > A.stack_cap - (kParkS ? kSumEntries : 0u)) atomicAdd(&A.counters[CNT_OVERFLOW], 1ull);
     }
   }
 }

@@ -216,6 +216,19 @@ int rc_pool_setting(bool *set = nullptr) {
   return n;
 }
 
+// rt_kernel_info of a run-time kernel from its code object's figures (rt_jit.cpp KernelMeta)
+void fill_kernel_info(const rt::KernelMeta &m, const std::string &compiler, rt_kernel_info *k) {
+  k->vgprs = m.vgprs;
+  k->agprs = m.agprs;
+  k->sgprs = m.sgprs;
+  k->scratch_bytes = m.scratch;
+  k->vgpr_spills = m.vgpr_spills;
+  k->sgpr_spills = m.sgpr_spills;
+  k->run_time = 1;
+  std::snprintf(k->compiler, sizeof k->compiler, "%s", compiler.c_str());
+  std::snprintf(k->loader, sizeof k->loader, "%s", rt::jit_compiler_where().c_str());
+}
+
 struct rt_context {
   int device = 0;
   int cu_count = 0;
@@ -323,6 +336,7 @@ struct rt_context {
   uint32_t used_rc_levels = 0;    // colour-stack levels the last render kept in LDS
   int jit_source = RT_JIT_NONE;   // last render: where its run-time kernels came from
   double jit_ms = 0.0;            // ... and the host time spent obtaining them
+  rt_kernel_info used_kernel{};   // the last render's render kernel (registers, scratch, spills, compiler)
 };
 
 extern "C" {
@@ -638,6 +652,11 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   if (!out_dev && p->row_count > 0) return RT_ERR_INVALID_ARG;
   DeviceGuard g(c->device);
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // Every frame reuses the context's buffers (work counters, tile order, colour stack, candidate lists, tile-major frame,
+  // RNG tables): a frame enqueued on another stream than the previous frame first waits for that frame's end, so
+  // alternating streams on one context is safe; frames on one stream are ordered by the stream itself
+  if (c->ev_recorded && stream != c->last_stream && hipStreamWaitEvent(s, c->ev[2], 0) != hipSuccess) return RT_ERR_HIP;
+  c->last_stream = stream;
   const uint32_t n = static_cast<uint32_t>(p->row_count) * static_cast<uint32_t>(p->width);
   const uint32_t mb = static_cast<uint8_t>(p->max_bounces);   // rc_stack.max_count is u8 (:220,1596)
   // a frame counts as rendered only once its whole sequence is enqueued: any failure below leaves
@@ -704,6 +723,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                        c->accel_w4 ? c->accel.wide_stack : 0u,
                                        c->mixed_ok ? c->img.stack_need + c->mixed.depth + 1 : 0u}) +
                              (c->accel_ok ? rt::kSumEntries : 0u);
+  // the verified walk's parked random_test (entries 0 and 1) and pixel sum (the top kSumEntries) must not overlap
+  if (c->accel_ok && stack_cap < rt::kSumEntries + 2u) return RT_ERR_STACK;
   // (+ the block's RNG slots, kRngSlotBytes: the "stack" region's fixed tail)
   const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2 + kRngSlotBytes;
   size_t stack_bytes = stackless ? kRngSlotBytes : full_stack_bytes;
@@ -755,7 +776,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   auto note_jit = [c](const rt::JitKernels &jk) {
     c->jit_source = std::max(c->jit_source, jk.source);
     c->jit_ms += jk.ms;
+    fill_kernel_info(c->counted ? jk.meta_count : jk.meta_render, jk.compiler, &c->used_kernel);
   };
+  c->used_kernel = rt_kernel_info{};
   c->used_fold = false;
   if (trav < 0 || trav == RT_TRAV_STATIC) {
     rt::JitKernels jk;
@@ -863,6 +886,16 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   rc_levels = (rc_levels + codes_per_word - 1) / codes_per_word * codes_per_word;   // whole LDS words per lane
   c->lds_bytes = static_cast<size_t>(scene_lds_words) * 4 + rc_levels * level_bytes + stack_bytes;
   c->used_traversal = trav;
+  if (!jit_fn) {   // an offline kernel of this library: its attributes (the allocator's spill counts are not among them)
+    int vg = -1, sc = -1;
+    rt::render_kernel_attrs(c->variant, &vg, &sc);
+    rt::KernelMeta m;
+    m.vgprs = vg;
+    m.scratch = sc;
+    fill_kernel_info(m, "", &c->used_kernel);
+    c->used_kernel.run_time = 0;
+    c->used_kernel.loader[0] = '\0';
+  }
   int per_cu = jit_fn ? rt::jit_blocks_per_cu(jit_fn, c->lds_bytes) : rt::render_blocks_per_cu(c->variant, c->lds_bytes);
   if (c->blocks_per_cu > 0) per_cu = std::min(c->blocks_per_cu, per_cu);   // fewer blocks: more LDS levels each
   if (c->rc_lds_auto) {
@@ -952,6 +985,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->lds_bytes += stage_slots ? stage_slots * kStageBlockBytes + kStageWaveExtraBytes : 0u;
   c->used_stage_slots = stage_slots;
   const uint32_t rc_lds_words = static_cast<uint32_t>(rc_levels * level_bytes / 4);
+  c->used_kernel.blocks_per_cu = c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu;
   uint64_t blocks = static_cast<uint64_t>(c->blocks_per_cu > 0 ? std::min(c->blocks_per_cu, per_cu) : per_cu) *
                     static_cast<uint64_t>(c->cu_count);
   const uint64_t needed = (static_cast<uint64_t>(n) + rt::kBlock - 1) / rt::kBlock;
@@ -963,8 +997,8 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                  trav, per_cu, static_cast<unsigned long long>(blocks), c->lds_bytes, scene_lds_words, rc_levels, stack_cap,
                  1u << c->tile_shift, 64u >> c->tile_shift, stage_slots, pool_chunks);
 
-  // tiles of 64 pixels (RenderArgs::tile_shift): 32x2 by default, so that every 128-B line of a 32-aligned float
-  // frame row belongs to one tile (RT_TILE_W = 8 / 16 / 32 / 64)
+  // tiles of 64 pixels (RenderArgs::tile_shift): 8x8 by default (kDefaultTileShift); RT_TILE_W = 16 / 32 / 64 gives wider
+  // tiles (32x2: every 128-B line of a 32-aligned float frame row belongs to one tile)
   const uint32_t tile_shift = c->tile_shift;
   const uint32_t tw = 1u << tile_shift, th = 64u >> tile_shift;
   const uint32_t tiles_x = (static_cast<uint32_t>(p->width) + tw - 1) / tw;
@@ -973,9 +1007,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   // per-pixel jumps — one nibble-table product each — run in the render kernel at tile pickup) and the per-wave
   // slots
   // The tables are rewritten in place when the geometry changes, so the upload is stream-ordered: an async copy on
-  // the frame's stream from pinned staging, after the previous frame's render (the same stream, or — a caller
-  // alternating streams on one context — its render-end event), so a frame still in flight keeps reading the
-  // table it was launched with (a blocking null-stream copy did not wait for non-blocking streams).
+  // the frame's stream from pinned staging, after the previous frame's render (stream order; a frame on another stream
+  // waited for the previous frame's end at entry), so a frame still in flight keeps reading the table it was launched
+  // with (a blocking null-stream copy did not wait for non-blocking streams).
   {
     // (phase width = the tile width: every lane of a tile applies the same column table)
     const uint64_t key[5] = {p->seed, static_cast<uint64_t>(p->width) | (static_cast<uint64_t>(tile_shift) << 32),
@@ -983,7 +1017,6 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                              static_cast<uint64_t>(p->row_count)};
     const int cols_key = p->width | static_cast<int>(tile_shift << 24);
     const bool rows_new = std::memcmp(key, c->rows_key, sizeof key) != 0, cols_new = c->cols_width != cols_key;
-    if ((rows_new || cols_new) && c->ev_recorded && hipStreamWaitEvent(s, c->ev[2], 0) != hipSuccess) return RT_ERR_HIP;
     auto upload = [s](DevBuf &dst, PinBuf &stage, const std::vector<uint32_t> &v) {
       const size_t n = v.size() * 4;
       if (dst.ensure(n) != hipSuccess || stage.stage(v.data(), n) != hipSuccess ||
@@ -1241,7 +1274,6 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   c->last_params = *p;
   c->last_out = out_dev;
   c->last_out8 = out8_dev;
-  c->last_stream = stream;
   c->rendered = true;
   return RT_OK;
 }
@@ -1264,6 +1296,7 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->tiled_out = c->used_tiled ? 1 : 0;
   st->jit_source = c->jit_source;
   st->jit_ms = c->jit_ms;
+  st->kernel = c->used_kernel;
   DeviceGuard g(c->device);
   if (hipEventSynchronize(c->ev[2]) != hipSuccess) return RT_ERR_HIP;
   if (c->used_fold) {
@@ -1412,8 +1445,11 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
   return ok ? RT_OK : RT_ERR_HIP;
 }
 
-int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap) {
-  if (!scene || !buf || cap == 0) return RT_ERR_INVALID_ARG;
+// the run-time source a render of `scene` would build for `traversal` (rt_kernel_source, rt_kernel_build); *img_out (if
+// non-null) receives the compiled scene, *accel_w0 (accel traversal) the source at the allocator's register choice
+static int kernel_source_impl(const rt_scene *scene, int traversal, int32_t max_bounces, std::string *out,
+                              rt::SceneImage *img_out, std::string *accel_w0) {
+  if (!scene) return RT_ERR_INVALID_ARG;
   rt::SceneImage img;
   int rc = rt::compile_scene(scene, &img);
   if (rc != RT_OK) return rc;
@@ -1449,6 +1485,7 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
     if (!rt::build_sphere_accel(img, kAccelMinSpheres, &a, &why)) return RT_ERR_UNSUPPORTED;
     const int wide = rt::accel_width() == 4 ? (rt::accel_quant() ? 2 : 1) : 0;
     src = rt::jit_accel_source(img, variant, rt::accel_waves(wide), wide);
+    if (accel_w0) *accel_w0 = rt::jit_accel_source(img, variant, 0, wide);
   } else if (traversal == RT_TRAV_MIXED) {
     rt::MixedAccel m;
     std::string why;
@@ -1459,7 +1496,41 @@ int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, 
   } else {
     return RT_ERR_INVALID_ARG;
   }
+  *out = src;
+  if (img_out) *img_out = std::move(img);
+  return RT_OK;
+}
+
+int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap) {
+  if (!scene || !buf || cap == 0) return RT_ERR_INVALID_ARG;
+  std::string src;
+  const int rc = kernel_source_impl(scene, traversal, max_bounces, &src, nullptr, nullptr);
+  if (rc != RT_OK) return rc;
   copy_out(src, buf, cap);
+  return RT_OK;
+}
+
+int rt_kernel_build(const rt_scene *scene, int traversal, int32_t max_bounces, rt_kernel_info *out) {
+  if (!scene || !out) return RT_ERR_INVALID_ARG;
+  *out = rt_kernel_info{};
+  std::string src, w0;
+  rt::SceneImage img;
+  const int rc = kernel_source_impl(scene, traversal, max_bounces, &src, &img, &w0);
+  if (rc != RT_OK) return rc;
+  const char *prefix = traversal == RT_TRAV_STATIC ? "rt_static" : traversal == RT_TRAV_ACCEL ? "rt_accel"
+                     : traversal == RT_TRAV_MIXED ? "rt_mixed" : "rt_lane";
+  const std::vector<std::string> extra = traversal == RT_TRAV_STATIC ? rt::static_sched(img)
+                                       : traversal == RT_TRAV_ACCEL ? rt::accel_sched() : std::vector<std::string>{};
+  rt::KernelMeta m;
+  std::string compiler, why;
+  if (!rt::jit_build_meta(src, prefix, extra, "gfx950", &m, &compiler, &why)) return RT_ERR_UNSUPPORTED;
+  // the verified walk's 6-wave request is kept only without scratch (rt_jit.cpp jit_accel_kernels): else the
+  // allocator's own build
+  if (traversal == RT_TRAV_ACCEL && !std::getenv("RT_ACCEL_WAVES") && rt::accel_waves() > 0 &&
+      !rt::accel_waves_build_kept(m.scratch) &&
+      !rt::jit_build_meta(w0, prefix, extra, "gfx950", &m, &compiler, &why))
+    return RT_ERR_UNSUPPORTED;
+  fill_kernel_info(m, compiler, out);
   return RT_OK;
 }
 

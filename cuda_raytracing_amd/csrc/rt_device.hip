@@ -376,4 +376,13 @@ int render_blocks_per_cu(int variant, size_t lds_bytes) {
   return n < 1 ? 1 : n;
 }
 
+// registers and scratch of an offline render kernel (rt_stats.kernel; spill counts are not in the attributes)
+bool render_kernel_attrs(int variant, int *vgprs, int *scratch) {
+  hipFuncAttributes fa;
+  if (variant < 0 || variant >= kKernels.n || hipFuncGetAttributes(&fa, kKernels.ptr[variant]) != hipSuccess) return false;
+  *vgprs = fa.numRegs;
+  *scratch = static_cast<int>(fa.localSizeBytes);
+  return true;
+}
+
 }  // namespace rt

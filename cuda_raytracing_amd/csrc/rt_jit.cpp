@@ -9,6 +9,7 @@
 
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -22,8 +23,10 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
+#include "code_object.h"
 #include "device/embedded_headers.inc"
 #include "rt_render.h"
 
@@ -49,6 +52,85 @@ std::string arch_of(int dev) {
 }
 
 }  // namespace
+
+// ---- the compiler of the run-time kernels ----------------------------------------------------------------
+// A process that imports torch before loading this library (every test, bench.py, smoke()) already holds torch's
+// bundled ROCm 7.0 HIP runtime, hipRTC and comgr under the same sonames (libhiprtc.so.7, libamd_comgr.so.3), so the
+// hipRTC this library links against resolves to those and compiles with their LLVM 20 (AMD clang 20, roc-7.0.2),
+// while a process without torch (bin/raytracing) compiles with /opt/rocm's (ROCm 7.2, AMD clang 22): the same scene
+// got different kernels depending on who loaded first.  And LLVM 20 miscompiles the verified sphere walk at its
+// 6-wave register budget: its register allocator splits the live ranges of the loop-carried pixel sum (and 12 other
+// values) around the camera-ray candidate-list loop and places the split copies at the top of the loop's exit block
+// ahead of that block's exec-mask restore (`s_or_b64 exec, exec, s[10:11]`), so only the lanes that ran the loop
+// execute them while the inverse copies run for every lane: the other lanes' sums rotate (x, y, z) -> (stale, x, y)
+// (profiles/r06_defect/: the LLVM-20 code object with that one instruction moved above the copies is exact,
+// LLVM 22's build of the same source is exact).  So the run-time kernels are compiled by /opt/rocm's hipRTC, loaded
+// with dlmopen into a link namespace of its own (its own comgr with it), whatever the process loaded before.
+// RT_JIT_COMPILER=process (A/B, diagnostics) uses the hipRTC the process resolved instead; RT_JIT_HIPRTC=<path>
+// names another libhiprtc.
+namespace {
+struct RtcApi {
+  hiprtcResult (*version)(int *, int *) = nullptr;
+  hiprtcResult (*create)(hiprtcProgram *, const char *, const char *, int, const char *const *, const char *const *) = nullptr;
+  hiprtcResult (*compile)(hiprtcProgram, int, const char *const *) = nullptr;
+  hiprtcResult (*log_size)(hiprtcProgram, size_t *) = nullptr;
+  hiprtcResult (*log)(hiprtcProgram, char *) = nullptr;
+  hiprtcResult (*code_size)(hiprtcProgram, size_t *) = nullptr;
+  hiprtcResult (*code)(hiprtcProgram, char *) = nullptr;
+  hiprtcResult (*destroy)(hiprtcProgram *) = nullptr;
+  std::string where;   // "dlmopen:<path>" or "process"
+};
+
+RtcApi process_rtc() {
+  RtcApi a;
+  a.version = hiprtcVersion; a.create = hiprtcCreateProgram; a.compile = hiprtcCompileProgram;
+  a.log_size = hiprtcGetProgramLogSize; a.log = hiprtcGetProgramLog; a.code_size = hiprtcGetCodeSize;
+  a.code = hiprtcGetCode; a.destroy = hiprtcDestroyProgram;
+  a.where = "process";
+  return a;
+}
+
+RtcApi load_rtc() {
+  const char *mode = std::getenv("RT_JIT_COMPILER");
+  if (mode && std::strcmp(mode, "process") == 0) return process_rtc();
+  std::string path;
+  if (const char *e = std::getenv("RT_JIT_HIPRTC"); e && e[0]) {
+    path = e;
+  } else {
+    const char *root = std::getenv("ROCM_PATH");
+    path = std::string(root && root[0] ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
+  }
+  void *h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    std::fprintf(stderr, "[rt] dlmopen(%s) failed (%s): run-time kernels compiled with the process's hipRTC\n", path.c_str(),
+                 dlerror());
+    return process_rtc();
+  }
+  RtcApi a;
+  bool ok = true;
+  auto sym = [&](auto &fp, const char *name) {
+    void *f = dlsym(h, name);
+    if (!f) ok = false;
+    fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(f);
+  };
+  sym(a.version, "hiprtcVersion"); sym(a.create, "hiprtcCreateProgram"); sym(a.compile, "hiprtcCompileProgram");
+  sym(a.log_size, "hiprtcGetProgramLogSize"); sym(a.log, "hiprtcGetProgramLog"); sym(a.code_size, "hiprtcGetCodeSize");
+  sym(a.code, "hiprtcGetCode"); sym(a.destroy, "hiprtcDestroyProgram");
+  if (!ok) {
+    std::fprintf(stderr, "[rt] %s lacks hipRTC entry points: run-time kernels compiled with the process's hipRTC\n", path.c_str());
+    return process_rtc();
+  }
+  a.where = "dlmopen:" + path;
+  return a;
+}
+
+const RtcApi &rtc() {
+  static const RtcApi a = load_rtc();
+  return a;
+}
+}  // namespace
+
+std::string jit_compiler_where() { return rtc().where; }
 
 std::vector<std::string> jit_extra_options() {
   std::vector<std::string> v;
@@ -115,31 +197,32 @@ std::vector<std::string> jit_options(const std::string &arch, const std::vector<
 
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log,
                  const std::vector<std::string> &extra) {
+  const RtcApi &R = rtc();
   hiprtcProgram prog;
   const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
   const char *hdr_names[] = {"rt_layout.h", "rt_body.h"};
-  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_static.hip", 2, hdr_src, hdr_names) != HIPRTC_SUCCESS) {
+  if (R.create(&prog, src.c_str(), "rt_static.hip", 2, hdr_src, hdr_names) != HIPRTC_SUCCESS) {
     if (log) *log = "hiprtcCreateProgram failed";
     return false;
   }
   const std::vector<std::string> o = jit_options(arch, extra);
   std::vector<const char *> opts;
   for (const std::string &x : o) opts.push_back(x.c_str());
-  const hiprtcResult r = hiprtcCompileProgram(prog, static_cast<int>(opts.size()), opts.data());
+  const hiprtcResult r = R.compile(prog, static_cast<int>(opts.size()), opts.data());
   bool ok = r == HIPRTC_SUCCESS;
   if (log) {
     size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
+    R.log_size(prog, &n);
     log->assign(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &(*log)[0]);
+    if (n) R.log(prog, &(*log)[0]);
   }
   if (ok) {
     size_t n = 0;
-    hiprtcGetCodeSize(prog, &n);
+    R.code_size(prog, &n);
     code->resize(n);
-    ok = n > 0 && hiprtcGetCode(prog, code->data()) == HIPRTC_SUCCESS;
+    ok = n > 0 && R.code(prog, code->data()) == HIPRTC_SUCCESS;
   }
-  hiprtcDestroyProgram(&prog);
+  R.destroy(&prog);
   if (ok) {
     if (const char *dir = std::getenv("RT_JIT_DUMP")) {   // diagnostics: source + code object
       const std::string base = std::string(dir) + "/rt_static_" + std::to_string(std::hash<std::string>()(src));
@@ -225,10 +308,10 @@ void disk_store(const std::string &dir, const std::string &path, const std::stri
 // built against, and the embedded device headers.
 std::string toolchain_tag() {
   int major = 0, minor = 0, runtime = 0;
-  hiprtcVersion(&major, &minor);
+  rtc().version(&major, &minor);
   if (hipRuntimeGetVersion(&runtime) != hipSuccess) runtime = -1;
   static const std::string headers = std::to_string(fnv1a(std::string(kEmbedLayout) + '\x01' + kEmbedBody));
-  return "hiprtc " + std::to_string(major) + "." + std::to_string(minor) + " runtime " + std::to_string(runtime) +
+  return "hiprtc " + rtc().where + " " + std::to_string(major) + "." + std::to_string(minor) + " runtime " + std::to_string(runtime) +
          " built " + std::to_string(HIP_VERSION_MAJOR) + "." + std::to_string(HIP_VERSION_MINOR) + "." +
          std::to_string(HIP_VERSION_PATCH) + " headers " + headers;
 }
@@ -263,7 +346,9 @@ bool build_module(const std::string &src, const std::string &prefix, JitKernels 
     }
     if (!have) {
       e->why = "hipRTC compile failed: " + log.substr(0, 2000);
-    } else if (hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
+    } else if ((code_object_kernel(code, prefix + "_render", &e->k.meta_render, &e->k.compiler),
+                code_object_kernel(code, prefix + "_render_count", &e->k.meta_count, nullptr),
+                hipModuleLoadData(&e->mod, code.data()) != hipSuccess) ||
                hipModuleGetFunction(&e->k.render, e->mod, (prefix + "_render").c_str()) != hipSuccess ||
                hipModuleGetFunction(&e->k.render_count, e->mod, (prefix + "_render_count").c_str()) != hipSuccess ||
                hipModuleGetFunction(&e->k.probe, e->mod, (prefix + "_probe").c_str()) != hipSuccess) {
@@ -514,6 +599,23 @@ constexpr int kAccelWavesScratchMax = 0;   // round 4: 96 B (see accel_waves)
 // +23 % under max-ilp, scene 0 level).  RT_ACCEL_SCHED=<strategy> overrides, RT_ACCEL_SCHED=0 keeps the default.
 std::vector<std::string> accel_sched() { return sched_options("RT_ACCEL_SCHED", true); }
 
+bool accel_waves_build_kept(int scratch_bytes) { return scratch_bytes >= 0 && scratch_bytes <= kAccelWavesScratchMax; }
+
+bool jit_build_meta(const std::string &src, const std::string &prefix, const std::vector<std::string> &extra,
+                    const std::string &arch, KernelMeta *m, std::string *compiler, std::string *why) {
+  std::vector<char> code;
+  std::string log;
+  if (!jit_compile(src, arch, &code, &log, extra)) {
+    if (why) *why = "hipRTC compile failed: " + log.substr(0, 2000);
+    return false;
+  }
+  if (!code_object_kernel(code, prefix + "_render", m, compiler)) {
+    if (why) *why = "no " + prefix + "_render in the code object's metadata";
+    return false;
+  }
+  return true;
+}
+
 bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
@@ -525,7 +627,7 @@ bool jit_accel_kernels(const SceneImage &img, int variant, int wide, JitKernels 
     render_vgprs(out->render, &sc);
     if (std::getenv("RT_DEBUG"))
       std::fprintf(stderr, "[rt] jit accel waves_per_eu(%d): scratch %d B per lane\n", w, sc);
-    if (sc < 0 || sc > kAccelWavesScratchMax) {
+    if (!accel_waves_build_kept(sc)) {
       JitKernels k = *out;
       if (!build_module(jit_accel_source(img, variant, 0, wide), "rt_accel", &k, why, sched)) return false;
       k.ms += out->ms;

@@ -5,6 +5,7 @@
 #include <string>
 #include <vector>
 
+#include "code_object.h"
 #include "gpu_scene.h"
 
 namespace rt {
@@ -17,6 +18,8 @@ struct JitKernels {
   bool folded = false;                   // primitive tests exactly folded (scene_codegen.cpp)
   int source = 0;                        // RT_JIT_MEMORY / RT_JIT_DISK / RT_JIT_COMPILED (rt_render.h)
   double ms = 0.0;                       // host time spent obtaining the module in this call
+  KernelMeta meta_render, meta_count;    // what the register allocator made of render / render_count (code object)
+  std::string compiler;                  // the compiler that built the module (its .comment line)
 };
 
 // Compile (or fetch from the process-wide cache) the StaticTrace kernels of `img` for `variant`
@@ -51,10 +54,24 @@ uint32_t scene_kinds(const SceneImage &img);
 // material / texture kinds present, as variant bits (kVarMatShift / kVarTexShift)
 int scene_shading_bits(const SceneImage &img);
 
+// where the run-time compiler comes from: "dlmopen:<libhiprtc path>" (default: /opt/rocm's, in a link namespace of
+// its own) or "process" (RT_JIT_COMPILER=process, or the fallback when that load fails)
+std::string jit_compiler_where();
+
 // extra hipRTC options from the RT_JIT_OPTS environment variable (space separated)
 std::vector<std::string> jit_extra_options();
 // the complete hipRTC option vector for `arch` (numerics flags + RT_JIT_OPTS); hashed into the disk-cache key
 std::vector<std::string> jit_options(const std::string &arch, const std::vector<std::string> &extra = {});
+
+// the machine-scheduler options of the scene-specialised kernels and of the verified sphere walk (RT_STATIC_SCHED,
+// RT_ACCEL_SCHED)
+std::vector<std::string> static_sched(const SceneImage &img);
+std::vector<std::string> accel_sched();
+// the verified walk's default waves request is kept only when its build has no more scratch than this (0)
+bool accel_waves_build_kept(int scratch_bytes);
+// compile `src` for `arch` with the run-time compiler and options (no device) and read <prefix>_render's figures
+bool jit_build_meta(const std::string &src, const std::string &prefix, const std::vector<std::string> &extra,
+                    const std::string &arch, KernelMeta *m, std::string *compiler, std::string *why);
 
 hipError_t jit_launch(hipFunction_t fn, const RenderArgs &a, uint32_t blocks, size_t lds_bytes, hipStream_t s);
 int jit_blocks_per_cu(hipFunction_t fn, size_t lds_bytes);

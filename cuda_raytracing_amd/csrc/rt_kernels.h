@@ -33,5 +33,7 @@ hipError_t launch_unpermute(const void *src, void *dst, uint32_t rows, uint32_t 
                             uint32_t row_bytes, hipStream_t s);
 // resident 256-thread blocks per CU for the chosen variant (occupancy query)
 int render_blocks_per_cu(int variant, size_t lds_bytes);
+// VGPRs and scratch bytes per lane of the offline render kernel of `variant` (false: unknown variant)
+bool render_kernel_attrs(int variant, int *vgprs, int *scratch);
 
 }  // namespace rt

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* status codes */
 #define RT_OK                 0
@@ -114,6 +114,22 @@ enum {
   RT_CNT__COUNT = 16
 };
 
+/* ABI 6: a render kernel as the register allocator built it.  Run-time (hipRTC) kernels: from the code object's
+ * metadata note (NT_AMDGPU_METADATA) and its .comment; offline kernels: hipFuncGetAttributes (spill counts -1). */
+typedef struct rt_kernel_info {
+  int32_t vgprs;           /* VGPRs per lane (the wave's residency follows from it, 512 / granule-rounded count) */
+  int32_t agprs;           /* AGPRs per lane (0: the path has no MFMA) */
+  int32_t sgprs;           /* SGPRs per wave */
+  int32_t scratch_bytes;   /* private segment per lane: > 0 means registers were spilled to memory */
+  int32_t vgpr_spills;     /* VGPRs the allocator spilled (-1: unknown) */
+  int32_t sgpr_spills;     /* SGPRs the allocator spilled (into VGPR lanes, or scratch) (-1: unknown) */
+  int32_t blocks_per_cu;   /* resident blocks per CU the launch used (0 if not launched) */
+  int32_t run_time;        /* 1: run-time compiled (hipRTC), 0: an offline kernel of librt_hip.so */
+  char compiler[128];      /* the compiler's identification ("AMD clang version ..."), "" if unknown */
+  char loader[128];        /* run-time kernels: where their hipRTC came from ("dlmopen:/opt/rocm/lib/libhiprtc.so.7" or
+                              "process"); offline kernels: "" */
+} rt_kernel_info;
+
 typedef struct rt_stats {
   double init_ms;          /* RNG seeding kernel (reference: init_gpu_data, untimed there) */
   double render_ms;        /* render kernel (the reference's "Rendering time" region, :1752-1768) */
@@ -147,6 +163,8 @@ typedef struct rt_stats {
   int32_t devices;         /* devices that rendered the frame (1 for the single-device entry points) */
   int32_t rc_pool_chunks;  /* deep colour-stack levels: LDS pool chunks per wave of the last render (0: levels past
                               rc_lds_levels in HBM only; RT_RC_POOL) */
+  /* ABI 6 */
+  rt_kernel_info kernel;   /* the last render's render kernel */
 } rt_stats;
 
 /* rt_stats.jit_source */
@@ -229,6 +247,11 @@ int rt_static_compile(const rt_scene *scene, uint32_t max_visits, const char *ar
  * would build it (traversal = RT_TRAV_STATIC, RT_TRAV_ACCEL, RT_TRAV_MIXED or RT_TRAV_LANE; no device
  * needed): ISA / register / scratch inspection with hipcc (tools/isa_stats.sh). */
 int rt_kernel_source(const rt_scene *scene, int traversal, int32_t max_bounces, char *buf, uint64_t cap);
+/* The render kernel that source compiles to (no device needed): rt_kernel_source's source built by the same run-time
+ * compiler, options and register-budget rules a render applies before its device-dependent residency step (the verified
+ * sphere walk's 6-wave request kept only without scratch).  Diagnostics and the CPU test that the default kernels of
+ * every BASELINE config build without spills. */
+int rt_kernel_build(const rt_scene *scene, int traversal, int32_t max_bounces, rt_kernel_info *out);
 /* Diagnostics for the verified mixed-world traversal (no device needed): info = {macro roots, dynamic
  * ones, primitives in their SAH trees, deepest SAH tree}; RT_ERR_UNSUPPORTED when no subtree qualifies.
  * The build reads the RT_MIX_* environment knobs (e.g. RT_MIX_DYN_MIN, the dynamic-macro primitive

@@ -23,7 +23,7 @@ def test_render_header_symbols():
     assert "rt_render" in names and "rt_context_render" in names
     for n in names:
         assert hasattr(lib, n), n
-    assert lib.rt_abi_version() == 5
+    assert lib.rt_abi_version() == 6
 
 
 def test_host_header_symbols():

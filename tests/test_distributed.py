@@ -57,6 +57,28 @@ def test_gather_rows_world2(H):
     assert result.get("equal_u8") is True
 
 
+@pytest.mark.parametrize("world,H", [(2, 22), (3, 31)])
+def test_bench_rank_path_gloo(tmp_path, world, H):
+    """bench.py's N>1 path end to end on CPU: launch_plan decides to spawn, spawn_ranks starts the ranks under
+    torch.distributed.run (127.0.0.1), each rank's rows go through bench.gather_frame (gloo), and rank 0's
+    bench.gather_check compares the assembled rows with the oracle's bytes (tests/dist_rank.py)."""
+    sys.path.insert(0, str(REPO))
+    import bench
+    assert bench.launch_plan(world, {}, world, "gloo") == ("spawn", world)
+    out = tmp_path / "chk.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "2"
+    rc = bench.spawn_ranks(world, [str(out), "40", str(H), "3", "5"], script=REPO / "tests" / "dist_rank.py", env=env)
+    assert rc == 0
+    import json
+    d = json.loads(out.read_text())
+    assert d["world_size"] == world
+    assert d["gather_bit_exact"] is True, d
+    assert d["whole_frame_equal"] is True
+    ranks = d["checked_rows"].split("ranks ")[1].rstrip(")")
+    assert ranks == str(list(range(world))), d   # the checked rows cover every rank's shard
+
+
 def test_weak_scaled_resolution():
     from cuda_raytracing_amd.multi_gpu import weak_scaled_resolution
     assert weak_scaled_resolution(1920, 1080, 1) == (1920, 1080)
