@@ -30,16 +30,24 @@ HIP_SRC  := $(CSRC)/rt_device.hip $(CSRC)/rt_capi.cpp $(CSRC)/scene_compile.cpp 
 HIP_HDR  := $(wildcard $(CSRC)/*.h) $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h \
             $(CSRC)/device/embedded_headers.inc include/rt_render.h include/rt_ref_layout.h
 
+# Each library records the hash of the sources it was built from (rt_hip_build_hash / rt_host_build_hash); the Python
+# binding recomputes it over the same files and refuses a library that does not match the tree, so a stale prebuilt
+# .so can never be what a test, smoke() or bench.py runs (build() is the only producer of the libraries they load)
+HIP_STAMP_SRC  := $(sort $(HIP_SRC) $(filter-out $(CSRC)/device/embedded_headers.inc,$(HIP_HDR)) $(CSRC)/jitc/rt_jitc.cpp)
+HOST_STAMP_SRC := $(sort $(HOST_SRC) $(CSRC)/host/glibc_rand.h $(CSRC)/host/image_decoders.h include/rt_host.h \
+                    include/rt_ref_layout.h include/rt_render.h)
+stamp = -DRT_SOURCE_HASH='"$(shell cat $(1) | sha256sum | cut -c1-16)"' -DRT_SOURCE_FILES='"$(1)"'
+
 all: host hip oracle cli ref
 
 host: $(LIBDIR)/librt_host.so
-hip: $(LIBDIR)/librt_hip.so
+hip: $(LIBDIR)/librt_hip.so $(LIBDIR)/rt_jitc
 oracle: oracle/_build/liboracle_rt.so
 cli: bin/raytracing
 
 $(LIBDIR)/librt_host.so: $(HOST_SRC) $(CSRC)/host/glibc_rand.h $(CSRC)/host/image_decoders.h include/rt_host.h include/rt_ref_layout.h include/rt_render.h
 	@mkdir -p $(LIBDIR)
-	$(CXX) $(HOST_FLAGS) $(INC) -shared $(HOST_SRC) -o $@
+	$(CXX) $(HOST_FLAGS) $(INC) $(call stamp,$(HOST_STAMP_SRC)) -shared $(HOST_SRC) -o $@
 
 # device headers embedded as text for the run-time (hipRTC) scene-specialised kernels
 $(CSRC)/device/embedded_headers.inc: $(CSRC)/device/rt_layout.h $(CSRC)/device/rt_body.h tools/embed_headers.py
@@ -47,7 +55,13 @@ $(CSRC)/device/embedded_headers.inc: $(CSRC)/device/rt_layout.h $(CSRC)/device/r
 
 $(LIBDIR)/librt_hip.so: $(HIP_SRC) $(HIP_HDR)
 	@mkdir -p $(LIBDIR)
-	$(HIPCC) $(HIP_FLAGS) $(INC) -shared $(HIP_SRC) -o $@ -L$(ROCM)/lib -lhiprtc -ldl
+	$(HIPCC) $(HIP_FLAGS) $(INC) $(call stamp,$(HIP_STAMP_SRC)) -shared $(HIP_SRC) -o $@ -L$(ROCM)/lib -lhiprtc -ldl
+
+# the run-time kernels' compiler process (rt_jit.cpp): /opt/rocm's hipRTC, whatever the calling process loaded
+$(LIBDIR)/rt_jitc: $(CSRC)/jitc/rt_jitc.cpp
+	@mkdir -p $(LIBDIR)
+	$(CXX) -O2 -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include $< -o $@ -L$(ROCM)/lib -lhiprtc \
+	  -Wl,-rpath,$(ROCM)/lib
 
 oracle/_build/liboracle_rt.so: oracle/oracle_rt.c include/rt_render.h include/rt_ref_layout.h
 	@mkdir -p oracle/_build
@@ -77,6 +91,6 @@ kat:
 	oracle/_build/gen_rocrand_kat > tests/golden/rng_kat.json
 
 clean:
-	rm -rf $(LIBDIR)/*.so oracle/_build bin
+	rm -rf $(LIBDIR)/*.so $(LIBDIR)/rt_jitc oracle/_build bin
 
 .PHONY: all host hip oracle cli ref kat clean

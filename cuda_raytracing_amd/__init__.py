@@ -25,7 +25,7 @@ __all__ = [
     "RT_FLAG_NO_JIT", "RT_FLAG_RC_AUDIT", "RT_FLAG_FORCE_MIXED", "RT_FLAG_NO_MIXED", "RT_TRAV_MIXED", "RT_FLAG_FORCE_LANE", "RT_FLAG_FORCE_PACKET", "RT_FLAG_FORCE_STATIC", "RT_FLAG_NO_FOLD", "RT_FLAG_FORCE_ACCEL", "RT_FLAG_NO_ACCEL", "RT_TRAV_ACCEL", "RT_TRAV_LANE",
     "RT_TRAV_PACKET", "RT_TRAV_STATIC", "static_source", "static_compile", "accel_build", "tonemap_device", "RT_SCENE_COUNT", "RT_SCENE_RANDOM_10K",
     "RT_XF_NONE", "RT_XF_TRANSLATE", "RT_XF_YROTATE", "RT_XF_YROTATE_TRANSLATE", "RenderError", "load_image",
-    "render_devices", "multi_row_map",
+    "render_devices", "multi_row_map", "kernel_build",
 ]
 
 
@@ -260,6 +260,14 @@ def render(scene: Scene, camera: Camera, params: Params, with_stats: bool = Fals
     _check(_abi.hip_lib().rt_render(C.byref(scene), C.byref(camera), C.byref(params),
                                     out.ctypes.data_as(C.c_void_p), C.byref(st)), "rt_render")
     return (out, st) if with_stats else out
+
+
+def kernel_build(scene: Scene, traversal: int, max_bounces: int) -> dict:
+    """rt_kernel_build: the render kernel a render of `scene` with `traversal` would build, compiled here by the run-time
+    compiler (no device): VGPRs, SGPRs, scratch bytes, spill counts, the compiler and where its hipRTC came from."""
+    k = _abi.KernelInfo()
+    _check(_abi.hip_lib().rt_kernel_build(C.byref(scene), traversal, max_bounces, C.byref(k)), "rt_kernel_build")
+    return k.as_dict()
 
 
 def render_devices(scene: Scene, camera: Camera, params: Params, devices, rgb: bool = True, ppm: bool = True,

@@ -24,6 +24,7 @@ RT_ERR_HIP = -3
 RT_ERR_NO_DEVICE = -4
 RT_ERR_STACK = -5
 RT_ERR_UNSUPPORTED = -6
+RT_ERR_DEVICE_CHECK = -7
 
 RT_FLAG_COUNT = 0x1
 RT_FLAG_GLOBAL_SCENE = 0x2
@@ -144,12 +145,37 @@ _hip = None
 _oracle = None
 
 
+def check_build_stamp(L, prefix: str, path: Path) -> None:
+    """Refuse a library built from other sources than this tree's (Makefile `stamp`): it records the files it was built
+    from and the sha256 of their bytes; recompute both here.  build() (make) is the only producer of the libraries the
+    tests, smoke() and bench.py load, so a stale prebuilt library fails loudly instead of being measured.
+    (RT_HIP_LIB — another build for a same-box A/B — is exempt.)"""
+    import hashlib
+    h = getattr(L, prefix + "_build_hash", None)
+    f = getattr(L, prefix + "_build_files", None)
+    if h is None or f is None:
+        raise RuntimeError(f"{path} carries no build stamp: rebuild with `make` / __graft_entry__.build()")
+    h.restype = C.c_char_p
+    f.restype = C.c_char_p
+    want, files = h().decode(), f().decode().split()
+    if want == "unstamped" or not files:
+        raise RuntimeError(f"{path} was built without a source stamp: rebuild with `make` / __graft_entry__.build()")
+    d = hashlib.sha256()
+    for name in files:
+        d.update((REPO_DIR / name).read_bytes())
+    got = d.hexdigest()[:16]
+    if got != want:
+        raise RuntimeError(f"{path} was built from other sources (stamp {want}, tree {got}): stale library; rebuild with "
+                           "`make` / __graft_entry__.build()")
+
+
 def host_lib():
     global _host
     if _host is None:
         if not HOST_LIB.exists():
             raise RuntimeError(f"{HOST_LIB} missing: run `make host` (or __graft_entry__.build())")
         L = C.CDLL(str(HOST_LIB))
+        check_build_stamp(L, "rt_host", HOST_LIB)
         P = C.c_void_p
         _sig(L.rt_world_create, P, C.c_uint32, C.c_uint64)
         _sig(L.rt_world_destroy, None, P)
@@ -195,7 +221,8 @@ HIP_SYMBOLS = ["rt_render", "rt_context_create", "rt_context_render", "rt_contex
                "rt_static_source", "rt_static_compile", "rt_context_note", "rt_tonemap_device", "rt_accel_build",
                "rt_seed_states", "rt_kernel_source", "rt_mixed_build", "rt_multi_create", "rt_multi_render",
                "rt_multi_destroy", "rt_render_devices", "rt_multi_row_map", "rt_accel_build_wide", "rt_rng_table_states",
-               "rt_accel_build_quant", "rt_prim_lists", "rt_multi_unpermute", "rt_kernel_build"]
+               "rt_accel_build_quant", "rt_prim_lists", "rt_multi_unpermute", "rt_kernel_build",
+               "rt_hip_build_hash", "rt_hip_build_files"]
 
 
 def _bind_single_hip_runtime():
@@ -221,6 +248,8 @@ def hip_lib():
                                "(run `make hip` / __graft_entry__.build()); there is no CPU fallback")
         _bind_single_hip_runtime()
         L = C.CDLL(str(HIP_LIB))
+        if not os.environ.get("RT_HIP_LIB"):
+            check_build_stamp(L, "rt_hip", HIP_LIB)
         P = C.c_void_p
 
         # (entry points added in ABI 5 are bound when present: RT_HIP_LIB may name an older build for an A/B)
@@ -298,7 +327,7 @@ def oracle_lib(path=None):
 
 def status_string(code: int) -> str:
     names = {0: "ok", -1: "invalid argument", -2: "malformed scene", -3: "HIP runtime error",
-             -4: "no HIP device", -5: "traversal stack too deep", -6: "unsupported"}
+             -4: "no HIP device", -5: "traversal stack too deep", -6: "unsupported", -7: "device check failed"}
     return names.get(code, f"status {code}")
 
 

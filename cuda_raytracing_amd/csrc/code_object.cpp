@@ -112,6 +112,7 @@ bool code_object_kernels(const std::vector<char> &co, std::vector<KernelMeta> *o
     const uint64_t h = shoff + static_cast<uint64_t>(k) * shentsize;
     Sec s{};
     if (!rd(co, h, &s.name) || !rd(co, h + 4, &s.type) || !rd(co, h + 24, &s.off) || !rd(co, h + 32, &s.size)) return false;
+    if (s.type == 8 /* SHT_NOBITS: no file bytes (.bss, .relro_padding) */ || s.type == 0) s.size = 0;
     if (s.off > co.size() || co.size() - s.off < s.size) return false;
     secs.push_back(s);
   }

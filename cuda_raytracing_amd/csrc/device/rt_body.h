@@ -81,6 +81,25 @@ struct Mem {
 };
 
 // ---------------------------------------------------------------------------------------------
+// device checks (RT_DEVICE_CHECKS builds; rt_layout.h CheckSite): RT_CHECK(A, cond, site, index, capacity) is true when
+// cond holds; otherwise the first failing site of the launch, its index and capacity go to work words kCheckWord..+2,
+// and the caller skips the access.  Without RT_DEVICE_CHECKS it is the constant true and compiles away.
+// ---------------------------------------------------------------------------------------------
+__device__ __noinline__ bool check_fail(const RenderArgs &A, uint32_t site, uint32_t index, uint32_t cap) {
+  if (atomicCAS(A.work + kCheckWord, 0u, site) == 0u) {
+    atomicExch(A.work + kCheckWord + 1, index);
+    atomicExch(A.work + kCheckWord + 2, cap);
+  }
+  return false;
+}
+#ifdef RT_DEVICE_CHECKS
+#define RT_CHECK(A, cond, site, index, cap) \
+  (__builtin_expect(!!(cond), 1) ? true : check_fail((A), (site), static_cast<uint32_t>(index), static_cast<uint32_t>(cap)))
+#else
+#define RT_CHECK(A, cond, site, index, cap) true
+#endif
+
+// ---------------------------------------------------------------------------------------------
 // RNG: rocRAND XORWOW (replaces cuRAND)
 // ---------------------------------------------------------------------------------------------
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); LLVM does not form it for
@@ -787,13 +806,21 @@ struct LaneTraceK {
       stk[0] = static_cast<uint16_t>(root);
       T.sp = 1;
     }
+    // the walk's share of the lane's stack: the verified sphere walk's fallback (TRACK) runs below its parked pixel sum
+    [[maybe_unused]] const uint32_t cap = A.stack_cap - (TRACK ? kSumEntries : 0u);
     if (!PAUSE) {
-      while (T.sp > 0) trav_step<LDS, COUNT, UV, KM, ALL, TRACK>(S, T, r, h, stk, vc);
+      while (T.sp > 0) {
+        trav_step<LDS, COUNT, UV, KM, ALL, TRACK>(S, T, r, h, stk, vc);
+        if (!RT_CHECK(A, T.sp <= cap, CHK_LANE_STACK, T.sp, cap)) T.sp = 0;
+      }
       return;
     }
     const uint32_t started = static_cast<uint32_t>(__popcll(__ballot(true)));
     for (uint32_t it = 1;; ++it) {
-      if (T.sp > 0) trav_step<LDS, COUNT, UV, KM, ALL>(S, T, r, h, stk, vc);
+      if (T.sp > 0) {
+        trav_step<LDS, COUNT, UV, KM, ALL>(S, T, r, h, stk, vc);
+        if (!RT_CHECK(A, T.sp <= cap, CHK_LANE_STACK, T.sp, cap)) T.sp = 0;
+      }
       const uint64_t left = __ballot(T.sp > 0);
       if (left == 0) break;
       const uint32_t nl = static_cast<uint32_t>(__popcll(left));
@@ -1112,6 +1139,7 @@ struct AccelTraceK {
             if (n_in >= 3) stk[(sp + n_in - 3) * 64] = static_cast<uint16_t>(key[2]);
             if (n_in >= 2) stk[(sp + n_in - 2) * 64] = static_cast<uint16_t>(key[1]);
             sp += n_in - 1;
+            if (!RT_CHECK(A, static_cast<uint32_t>(sp) <= A.stack_cap - kSumEntries, CHK_ACCEL_STACK, sp, A.stack_cap - kSumEntries)) sp = 0;
             node = key[0] & 0xffffu;
           } else if (sp == 0) {
             walking = false;
@@ -1155,6 +1183,7 @@ struct AccelTraceK {
         if (hn && hf) {
           stk[sp * 64] = static_cast<uint16_t>(rf);
           ++sp;
+          if (!RT_CHECK(A, static_cast<uint32_t>(sp) <= A.stack_cap - kSumEntries, CHK_ACCEL_STACK, sp, A.stack_cap - kSumEntries)) sp = 0;
           node = rn;
         } else if (hn | hf) {
           node = hn ? rn : rf;
@@ -1540,6 +1569,7 @@ struct MixedTraceK {
             }
           }
         }
+        if (!RT_CHECK(A, static_cast<uint32_t>(sp) <= A.stack_cap, CHK_MIXED_STACK, sp, A.stack_cap)) sp = 0;
         T.sp = sp;
         continue;
       }
@@ -1593,6 +1623,7 @@ struct MixedTraceK {
       if (hn && hf) {
         stk[(T.sp + msp) * 64] = static_cast<uint16_t>(rf);
         ++msp;
+        if (!RT_CHECK(A, T.sp + msp <= A.stack_cap, CHK_MIXED_STACK, T.sp + msp, A.stack_cap)) msp = 0;
         mnode = rn;
         continue;
       }
@@ -1642,6 +1673,7 @@ struct MixedTraceK {
           for (uint32_t i = 0; i < w0.z; ++i) stk[(sp + i) * 64] = static_cast<uint16_t>(w0.y + i);
           sp += w0.z;
         }
+        if (!RT_CHECK(A, static_cast<uint32_t>(sp) <= A.stack_cap, CHK_MIXED_STACK, sp, A.stack_cap)) sp = 0;
         T.sp = sp;
       }
     }
@@ -1909,9 +1941,14 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     __threadfence_block();
   }
   auto rc_deep_store = [&](uint32_t k, uint32_t code) {
+    if (!RT_CHECK(A, k < mb, CHK_RC_DEEP, k, mb)) return;
     if constexpr (POOL) {
       const uint32_t c = *pool_lane;
-      if (c != 0xffu) { pool[kRcPoolHead + c * pool_stride + (k - A.rc_lds_levels)] = code; return; }
+      if (c != 0xffu) {
+        if (RT_CHECK(A, c < A.rc_pool_chunks, CHK_POOL_CHUNK, c, A.rc_pool_chunks))
+          pool[kRcPoolHead + c * pool_stride + (k - A.rc_lds_levels)] = code;
+        return;
+      }
     }
     rc_hbm_store(k, code);
   };
@@ -2497,7 +2534,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         // lights never scatter, raytracing.cu:439-450 vs :457-488, so the unwind adds +0.0f per level)
         if (push) {
           if (RC_LDS || rsp < A.rc_lds_levels) {
-            rc_lds_store(rsp, code);
+            if (RT_CHECK(A, rsp < A.rc_lds_levels, CHK_RC_LDS, rsp, A.rc_lds_levels)) rc_lds_store(rsp, code);
           } else {
             if constexpr (POOL) {
               // the lanes starting their first deep level this round take the lowest free chunks, one each in lane order
@@ -2635,10 +2672,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           const uint32_t tile = (plr >> tsh) * A.tiles_x + (pj >> ts);
           const uint32_t k = ((plr & ((1u << tsh) - 1u)) << ts) | (pj & twm);
           float *o = A.out + static_cast<size_t>(tile) * 192u + 3u * k;
-          o[0] = c.x;
-          o[1] = c.y;
-          o[2] = c.z;
-        } else {
+          if (RT_CHECK(A, tile * 64u + k < A.n_ids, CHK_PIXEL, tile * 64u + k, A.n_ids)) {
+            o[0] = c.x;
+            o[1] = c.y;
+            o[2] = c.z;
+          }
+        } else if (RT_CHECK(A, plr < A.rows && pj < static_cast<uint32_t>(A.width), CHK_PIXEL, pxy, (A.rows << 16) | A.width)) {
           const size_t pix = static_cast<size_t>(plr) * static_cast<uint32_t>(A.width) + pj;
           float *o = A.out + 3 * pix;
           o[0] = c.x;

@@ -304,6 +304,21 @@ constexpr uint32_t kStageFree = 0xffffffffu;
 constexpr uint32_t kStageSlotsMax = 4;
 constexpr uint32_t kXcdClasses = 8, kClsWord = 36;   // (work words 16..35: the mixed walk's RT_MIX_DIAG counters)
 constexpr uint32_t kTailWord = 44;                   // work word of the tail pieces' counter
+// Device checks (kernels built with RT_DEVICE_CHECKS: RT_CHECKS=1, rt_capi.cpp): the first index found out of its
+// capacity leaves {site, index, capacity} in work words kCheckWord..+2 and its access is skipped; the host then fails
+// the frame with RT_ERR_DEVICE_CHECK naming the site (rt_context_note).  (work words 48..51: the kernel span)
+constexpr uint32_t kCheckWord = 52;
+enum CheckSite : uint32_t {
+  CHK_NONE = 0,
+  CHK_LANE_STACK = 1,      // per-lane DFS stack pointer vs the lane's stack capacity (the walk's share of it)
+  CHK_ACCEL_STACK = 2,     // verified sphere walk's stack vs stack_cap - kSumEntries (the parked pixel sum above it)
+  CHK_MIXED_STACK = 3,     // verified mixed walk's reference stack + macro SAH stack vs stack_cap
+  CHK_RC_LDS = 4,          // colour-stack level stored in LDS vs rc_lds_levels
+  CHK_RC_DEEP = 5,         // colour-stack level past the LDS ones vs max_bounces
+  CHK_POOL_CHUNK = 6,      // a lane's deep-level pool chunk vs rc_pool_chunks
+  CHK_PIXEL = 7,           // output pixel / tile index vs the frame
+  CHK__COUNT = 8
+};
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile
 constexpr uint32_t kRcLdsLevels = 4;    // colour-stack levels kept in LDS (deeper ones spill to HBM)

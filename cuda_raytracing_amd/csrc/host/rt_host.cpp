@@ -899,6 +899,14 @@ int rt_write_ppm(const char *path, const float *rgb, uint32_t width, uint32_t he
   return n == bytes.size() ? RT_OK : RT_ERR_INVALID_ARG;
 }
 
+#ifndef RT_SOURCE_HASH
+#define RT_SOURCE_HASH "unstamped"
+#define RT_SOURCE_FILES ""
+#endif
+// the sources this library was built from and the hash of their bytes (Makefile `stamp`; checked by _abi.py)
+const char *rt_host_build_hash(void) { return RT_SOURCE_HASH; }
+const char *rt_host_build_files(void) { return RT_SOURCE_FILES; }
+
 int rt_abi_struct_sizes(uint32_t *out, int n) {
   const uint32_t v[8] = {sizeof(rt_scene), sizeof(rt_camera), sizeof(rt_params), sizeof(rt_stats),
                          sizeof(rt_settings), sizeof(rtr_hittable), sizeof(rtr_material), sizeof(rtr_texture)};

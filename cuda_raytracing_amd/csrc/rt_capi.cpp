@@ -343,6 +343,15 @@ extern "C" {
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 
+#ifndef RT_SOURCE_HASH
+#define RT_SOURCE_HASH "unstamped"
+#define RT_SOURCE_FILES ""
+#endif
+// the sources this library was built from and the hash of their bytes (Makefile `stamp`; cuda_raytracing_amd/_abi.py
+// refuses a library whose hash does not match the tree's files)
+const char *rt_hip_build_hash(void) { return RT_SOURCE_HASH; }
+const char *rt_hip_build_files(void) { return RT_SOURCE_FILES; }
+
 int rt_accel_build(const rt_scene *scene, uint32_t *words, uint64_t cap, uint32_t info[4]) {
   if (!scene || !info) return RT_ERR_INVALID_ARG;
   rt::SceneImage img;
@@ -465,6 +474,7 @@ const char *rt_status_string(int s) {
     case RT_ERR_NO_DEVICE: return "no HIP device";
     case RT_ERR_STACK: return "traversal stack too deep";
     case RT_ERR_UNSUPPORTED: return "unsupported";
+    case RT_ERR_DEVICE_CHECK: return "device check failed";
   }
   return "unknown status";
 }
@@ -725,6 +735,12 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                              (c->accel_ok ? rt::kSumEntries : 0u);
   // the verified walk's parked random_test (entries 0 and 1) and pixel sum (the top kSumEntries) must not overlap
   if (c->accel_ok && stack_cap < rt::kSumEntries + 2u) return RT_ERR_STACK;
+  // test aid of the device checks (RT_CHECKS=1 only): a per-lane stack RT_CHECK_STACK_CAP entries deep, too shallow on
+  // purpose, so the checks' naming of an overflow can be tested (tests/test_gpu_kernels.py)
+  uint32_t stack_cap_launch = stack_cap;
+  if (const char *ce = std::getenv("RT_CHECKS"); ce && ce[0] == '1')
+    if (const char *e = std::getenv("RT_CHECK_STACK_CAP"); e && std::atoi(e) > 0)
+      stack_cap_launch = std::min<uint32_t>(stack_cap, static_cast<uint32_t>(std::atoi(e)));
   // (+ the block's RNG slots, kRngSlotBytes: the "stack" region's fixed tail)
   const size_t full_stack_bytes = static_cast<size_t>(rt::kWavesPerBlock) * stack_cap * 64 * 2 + kRngSlotBytes;
   size_t stack_bytes = stackless ? kRngSlotBytes : full_stack_bytes;
@@ -1061,7 +1077,7 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   a.off_pixels = c->img.off_pixels;
   a.pixel_words = static_cast<uint32_t>(c->img.words.size()) - c->img.off_pixels;
   a.root = c->img.root;
-  a.stack_cap = stack_cap;
+  a.stack_cap = stack_cap_launch;
   a.accel_nodes = c->accel_nodes;
   a.accel_prims = c->accel_prims;
   a.accel_root = c->accel.root;
@@ -1339,6 +1355,22 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
   st->render_ms = d;
   st->samples = c->samples;
   st->devices = 1;
+  {   // device checks (RT_CHECKS=1 builds): the first index a kernel found out of its capacity fails the frame, named
+    uint32_t ck[3] = {0, 0, 0};
+    if (hipMemcpy(ck, static_cast<uint32_t *>(c->work.p) + rt::kCheckWord, sizeof ck, hipMemcpyDeviceToHost) != hipSuccess)
+      return RT_ERR_HIP;
+    if (ck[0] != rt::CHK_NONE) {
+      static const char *const names[rt::CHK__COUNT] = {"none", "lane DFS stack", "verified sphere walk stack",
+                                                        "verified mixed walk stack", "colour-stack LDS level",
+                                                        "colour-stack deep level", "deep-level pool chunk", "output pixel"};
+      char b[200];
+      std::snprintf(b, sizeof b, "device check failed: %s index %u >= capacity %u (site %u)",
+                    ck[0] < rt::CHK__COUNT ? names[ck[0]] : "unknown", ck[1], ck[2], ck[0]);
+      c->jit_why = b;
+      if (std::getenv("RT_DEBUG")) std::fprintf(stderr, "[rt] %s\n", b);
+      return RT_ERR_DEVICE_CHECK;
+    }
+  }
   {   // the render kernel's own span (RenderArgs::span): first wave start to last wave end
     unsigned long long sp[2] = {0, 0};
     if (hipMemcpy(sp, static_cast<uint32_t *>(c->work.p) + kSpanWord, sizeof sp, hipMemcpyDeviceToHost) != hipSuccess)
@@ -1523,13 +1555,17 @@ int rt_kernel_build(const rt_scene *scene, int traversal, int32_t max_bounces, r
                                        : traversal == RT_TRAV_ACCEL ? rt::accel_sched() : std::vector<std::string>{};
   rt::KernelMeta m;
   std::string compiler, why;
-  if (!rt::jit_build_meta(src, prefix, extra, "gfx950", &m, &compiler, &why)) return RT_ERR_UNSUPPORTED;
+  auto fail = [&why]() {
+    if (std::getenv("RT_DEBUG")) std::fprintf(stderr, "[rt] rt_kernel_build: %s\n", why.c_str());
+    return RT_ERR_UNSUPPORTED;
+  };
+  if (!rt::jit_build_meta(src, prefix, extra, "gfx950", &m, &compiler, &why)) return fail();
   // the verified walk's 6-wave request is kept only without scratch (rt_jit.cpp jit_accel_kernels): else the
   // allocator's own build
   if (traversal == RT_TRAV_ACCEL && !std::getenv("RT_ACCEL_WAVES") && rt::accel_waves() > 0 &&
       !rt::accel_waves_build_kept(m.scratch) &&
       !rt::jit_build_meta(w0, prefix, extra, "gfx950", &m, &compiler, &why))
-    return RT_ERR_UNSUPPORTED;
+    return fail();
   fill_kernel_info(m, compiler, out);
   return RT_OK;
 }

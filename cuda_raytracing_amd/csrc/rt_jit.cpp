@@ -10,7 +10,10 @@
 #include <hip/hiprtc.h>
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <spawn.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -23,7 +26,6 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <type_traits>
 #include <vector>
 
 #include "code_object.h"
@@ -64,73 +66,152 @@ std::string arch_of(int dev) {
 // ahead of that block's exec-mask restore (`s_or_b64 exec, exec, s[10:11]`), so only the lanes that ran the loop
 // execute them while the inverse copies run for every lane: the other lanes' sums rotate (x, y, z) -> (stale, x, y)
 // (profiles/r06_defect/: the LLVM-20 code object with that one instruction moved above the copies is exact,
-// LLVM 22's build of the same source is exact).  So the run-time kernels are compiled by /opt/rocm's hipRTC, loaded
-// with dlmopen into a link namespace of its own (its own comgr with it), whatever the process loaded before.
-// RT_JIT_COMPILER=process (A/B, diagnostics) uses the hipRTC the process resolved instead; RT_JIT_HIPRTC=<path>
-// names another libhiprtc.
+// LLVM 22's build of the same source is exact).  So the run-time kernels are compiled by rt_jitc, a small program next
+// to this library linked against /opt/rocm's hipRTC, started as a child process (posix_spawn; no torch in its address
+// space).  (A link namespace of its own — dlmopen of /opt/rocm's libhiprtc — gave the same compiler but crashed
+// inside comgr once other libraries had been loaded after it: a second libc in one process.)
+// RT_JIT_COMPILER=process (A/B, diagnostics) compiles in this process with the hipRTC it resolved; RT_JITC=<path>
+// names another helper.
 namespace {
-struct RtcApi {
-  hiprtcResult (*version)(int *, int *) = nullptr;
-  hiprtcResult (*create)(hiprtcProgram *, const char *, const char *, int, const char *const *, const char *const *) = nullptr;
-  hiprtcResult (*compile)(hiprtcProgram, int, const char *const *) = nullptr;
-  hiprtcResult (*log_size)(hiprtcProgram, size_t *) = nullptr;
-  hiprtcResult (*log)(hiprtcProgram, char *) = nullptr;
-  hiprtcResult (*code_size)(hiprtcProgram, size_t *) = nullptr;
-  hiprtcResult (*code)(hiprtcProgram, char *) = nullptr;
-  hiprtcResult (*destroy)(hiprtcProgram *) = nullptr;
-  std::string where;   // "dlmopen:<path>" or "process"
+std::string helper_path() {
+  if (const char *e = std::getenv("RT_JITC"); e && e[0]) return e;
+  Dl_info di;
+  if (dladdr(reinterpret_cast<void *>(&helper_path), &di) && di.dli_fname) {
+    const std::string p = di.dli_fname;
+    const size_t s = p.rfind('/');
+    return (s == std::string::npos ? std::string(".") : p.substr(0, s)) + "/rt_jitc";
+  }
+  return "rt_jitc";
+}
+
+// run the helper with `args`; its exit status (-1: it could not be started)
+int run_helper(const std::string &exe, const std::vector<std::string> &args, const std::string &out_file = "") {
+  std::vector<char *> argv;
+  argv.push_back(const_cast<char *>(exe.c_str()));
+  for (const std::string &a : args) argv.push_back(const_cast<char *>(a.c_str()));
+  argv.push_back(nullptr);
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  if (!out_file.empty()) posix_spawn_file_actions_addopen(&fa, 1, out_file.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  pid_t pid = 0;
+  const int e = posix_spawn(&pid, exe.c_str(), &fa, nullptr, argv.data(), environ);
+  posix_spawn_file_actions_destroy(&fa);
+  if (e != 0) return -1;
+  int status = 0;
+  while (waitpid(pid, &status, 0) < 0)
+    if (errno != EINTR) return -1;
+  return WIFEXITED(status) ? WEXITSTATUS(status) : -1;
+}
+
+bool write_file(const std::string &p, const std::string &data) {
+  FILE *f = std::fopen(p.c_str(), "wb");
+  if (!f) return false;
+  const bool ok = std::fwrite(data.data(), 1, data.size(), f) == data.size();
+  return (std::fclose(f) == 0) && ok;
+}
+bool read_file(const std::string &p, std::string *out) {
+  FILE *f = std::fopen(p.c_str(), "rb");
+  if (!f) return false;
+  out->clear();
+  char buf[1 << 16];
+  for (size_t n; (n = std::fread(buf, 1, sizeof buf, f)) > 0;) out->append(buf, n);
+  std::fclose(f);
+  return true;
+}
+
+struct Compiler {
+  bool helper = false;
+  std::string exe;
+  std::string where;     // "helper:<path>" or "process"
+  int major = 0, minor = 0;
 };
 
-RtcApi process_rtc() {
-  RtcApi a;
-  a.version = hiprtcVersion; a.create = hiprtcCreateProgram; a.compile = hiprtcCompileProgram;
-  a.log_size = hiprtcGetProgramLogSize; a.log = hiprtcGetProgramLog; a.code_size = hiprtcGetCodeSize;
-  a.code = hiprtcGetCode; a.destroy = hiprtcDestroyProgram;
-  a.where = "process";
-  return a;
+const Compiler &compiler() {
+  static const Compiler c = [] {
+    Compiler k;
+    const char *mode = std::getenv("RT_JIT_COMPILER");
+    if (!(mode && std::strcmp(mode, "process") == 0)) {
+      k.exe = helper_path();
+      char tmpl[] = "/tmp/rt_jitc_vXXXXXX";
+      const int fd = mkstemp(tmpl);
+      if (fd >= 0) {
+        close(fd);
+        std::string v;
+        if (access(k.exe.c_str(), X_OK) == 0 && run_helper(k.exe, {"--version"}, tmpl) == 0 && read_file(tmpl, &v) &&
+            std::sscanf(v.c_str(), "%d %d", &k.major, &k.minor) == 2) {
+          k.helper = true;
+          k.where = "helper:" + k.exe;
+        }
+        std::remove(tmpl);
+      }
+      if (!k.helper)
+        std::fprintf(stderr, "[rt] the kernel compiler %s could not be run: run-time kernels compiled with the process's "
+                     "hipRTC\n", k.exe.c_str());
+    }
+    if (!k.helper) {
+      hiprtcVersion(&k.major, &k.minor);
+      k.where = "process";
+    }
+    return k;
+  }();
+  return c;
 }
 
-RtcApi load_rtc() {
-  const char *mode = std::getenv("RT_JIT_COMPILER");
-  if (mode && std::strcmp(mode, "process") == 0) return process_rtc();
-  std::string path;
-  if (const char *e = std::getenv("RT_JIT_HIPRTC"); e && e[0]) {
-    path = e;
-  } else {
-    const char *root = std::getenv("ROCM_PATH");
-    path = std::string(root && root[0] ? root : "/opt/rocm") + "/lib/libhiprtc.so.7";
+bool compile_in_process(const std::string &src, const std::vector<std::string> &o, std::vector<char> *code,
+                        std::string *log) {
+  hiprtcProgram prog;
+  const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
+  const char *hdr_names[] = {"rt_layout.h", "rt_body.h"};
+  if (hiprtcCreateProgram(&prog, src.c_str(), "rt_static.hip", 2, hdr_src, hdr_names) != HIPRTC_SUCCESS) {
+    if (log) *log = "hiprtcCreateProgram failed";
+    return false;
   }
-  void *h = dlmopen(LM_ID_NEWLM, path.c_str(), RTLD_NOW | RTLD_LOCAL);
-  if (!h) {
-    std::fprintf(stderr, "[rt] dlmopen(%s) failed (%s): run-time kernels compiled with the process's hipRTC\n", path.c_str(),
-                 dlerror());
-    return process_rtc();
+  std::vector<const char *> opts;
+  for (const std::string &x : o) opts.push_back(x.c_str());
+  bool ok = hiprtcCompileProgram(prog, static_cast<int>(opts.size()), opts.data()) == HIPRTC_SUCCESS;
+  if (log) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    log->assign(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &(*log)[0]);
   }
-  RtcApi a;
-  bool ok = true;
-  auto sym = [&](auto &fp, const char *name) {
-    void *f = dlsym(h, name);
-    if (!f) ok = false;
-    fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(f);
-  };
-  sym(a.version, "hiprtcVersion"); sym(a.create, "hiprtcCreateProgram"); sym(a.compile, "hiprtcCompileProgram");
-  sym(a.log_size, "hiprtcGetProgramLogSize"); sym(a.log, "hiprtcGetProgramLog"); sym(a.code_size, "hiprtcGetCodeSize");
-  sym(a.code, "hiprtcGetCode"); sym(a.destroy, "hiprtcDestroyProgram");
-  if (!ok) {
-    std::fprintf(stderr, "[rt] %s lacks hipRTC entry points: run-time kernels compiled with the process's hipRTC\n", path.c_str());
-    return process_rtc();
+  if (ok) {
+    size_t n = 0;
+    hiprtcGetCodeSize(prog, &n);
+    code->resize(n);
+    ok = n > 0 && hiprtcGetCode(prog, code->data()) == HIPRTC_SUCCESS;
   }
-  a.where = "dlmopen:" + path;
-  return a;
+  hiprtcDestroyProgram(&prog);
+  return ok;
 }
 
-const RtcApi &rtc() {
-  static const RtcApi a = load_rtc();
-  return a;
+bool compile_in_helper(const std::string &exe, const std::string &src, const std::vector<std::string> &o,
+                       std::vector<char> *code, std::string *log) {
+  const char *td = std::getenv("TMPDIR");
+  std::string tmpl = std::string(td && td[0] ? td : "/tmp") + "/rt_jitc_XXXXXX";
+  if (!mkdtemp(&tmpl[0])) {
+    if (log) *log = "mkdtemp failed";
+    return false;
+  }
+  const std::string dir = tmpl;
+  std::string opts;
+  for (const std::string &x : o) opts += x + "\n";
+  const char *files[] = {"/src.hip", "/rt_layout.h", "/rt_body.h", "/opts.txt", "/code.co", "/log.txt"};
+  bool ok = write_file(dir + files[0], src) && write_file(dir + files[1], kEmbedLayout) &&
+            write_file(dir + files[2], kEmbedBody) && write_file(dir + files[3], opts);
+  const int rc = ok ? run_helper(exe, {dir}) : 2;
+  std::string lg, co;
+  read_file(dir + "/log.txt", &lg);
+  ok = rc == 0 && read_file(dir + "/code.co", &co) && !co.empty();
+  if (log) *log = rc < 0 ? "the kernel compiler " + exe + " could not be started" : lg;
+  if (ok) code->assign(co.begin(), co.end());
+  for (const char *f : files) std::remove((dir + f).c_str());
+  rmdir(dir.c_str());
+  return ok;
 }
 }  // namespace
 
-std::string jit_compiler_where() { return rtc().where; }
+std::string jit_compiler_where() { return compiler().where; }
 
 std::vector<std::string> jit_extra_options() {
   std::vector<std::string> v;
@@ -190,39 +271,23 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
 std::vector<std::string> jit_options(const std::string &arch, const std::vector<std::string> &extra) {
   std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                                 "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
+  // Loops are unrolled only where the source asks (#pragma unroll): ROCm 7.2's LLVM 22 otherwise also unrolls the
+  // colour-stack unwind and the rejection loops of the scene-specialised kernels (+11 % static VALU instructions, scene 0
+  // render +4 % against the LLVM 20 build; without: level, profiles/r06_ab_unroll_*.jsonl).  RT_JIT_UNROLL=1 (A/B)
+  // lets the unroller choose.
+  if (const char *e = std::getenv("RT_JIT_UNROLL"); !(e && e[0] == '1')) o.push_back("-fno-unroll-loops");
   for (const std::string &x : jit_extra_options()) o.push_back(x);
   for (const std::string &x : extra) o.push_back(x);
+  // RT_CHECKS=1: the run-time kernels with device bounds checks (rt_body.h RT_CHECK; diagnostics, debug builds)
+  if (const char *e = std::getenv("RT_CHECKS"); e && e[0] == '1') o.push_back("-DRT_DEVICE_CHECKS");
   return o;
 }
 
 bool jit_compile(const std::string &src, const std::string &arch, std::vector<char> *code, std::string *log,
                  const std::vector<std::string> &extra) {
-  const RtcApi &R = rtc();
-  hiprtcProgram prog;
-  const char *hdr_src[] = {kEmbedLayout, kEmbedBody};
-  const char *hdr_names[] = {"rt_layout.h", "rt_body.h"};
-  if (R.create(&prog, src.c_str(), "rt_static.hip", 2, hdr_src, hdr_names) != HIPRTC_SUCCESS) {
-    if (log) *log = "hiprtcCreateProgram failed";
-    return false;
-  }
+  const Compiler &C = compiler();
   const std::vector<std::string> o = jit_options(arch, extra);
-  std::vector<const char *> opts;
-  for (const std::string &x : o) opts.push_back(x.c_str());
-  const hiprtcResult r = R.compile(prog, static_cast<int>(opts.size()), opts.data());
-  bool ok = r == HIPRTC_SUCCESS;
-  if (log) {
-    size_t n = 0;
-    R.log_size(prog, &n);
-    log->assign(n, '\0');
-    if (n) R.log(prog, &(*log)[0]);
-  }
-  if (ok) {
-    size_t n = 0;
-    R.code_size(prog, &n);
-    code->resize(n);
-    ok = n > 0 && R.code(prog, code->data()) == HIPRTC_SUCCESS;
-  }
-  R.destroy(&prog);
+  const bool ok = C.helper ? compile_in_helper(C.exe, src, o, code, log) : compile_in_process(src, o, code, log);
   if (ok) {
     if (const char *dir = std::getenv("RT_JIT_DUMP")) {   // diagnostics: source + code object
       const std::string base = std::string(dir) + "/rt_static_" + std::to_string(std::hash<std::string>()(src));
@@ -307,11 +372,11 @@ void disk_store(const std::string &dir, const std::string &path, const std::stri
 // version (it carries the patch level, i.e. the bundled compiler build), the version this library was
 // built against, and the embedded device headers.
 std::string toolchain_tag() {
-  int major = 0, minor = 0, runtime = 0;
-  rtc().version(&major, &minor);
+  const int major = compiler().major, minor = compiler().minor;
+  int runtime = 0;
   if (hipRuntimeGetVersion(&runtime) != hipSuccess) runtime = -1;
   static const std::string headers = std::to_string(fnv1a(std::string(kEmbedLayout) + '\x01' + kEmbedBody));
-  return "hiprtc " + rtc().where + " " + std::to_string(major) + "." + std::to_string(minor) + " runtime " + std::to_string(runtime) +
+  return "hiprtc " + compiler().where + " " + std::to_string(major) + "." + std::to_string(minor) + " runtime " + std::to_string(runtime) +
          " built " + std::to_string(HIP_VERSION_MAJOR) + "." + std::to_string(HIP_VERSION_MINOR) + "." +
          std::to_string(HIP_VERSION_PATCH) + " headers " + headers;
 }
@@ -521,10 +586,11 @@ std::vector<std::string> sched_options(const char *env, bool on) {
   return {"-mllvm", "-amdgpu-sched-strategy=" + s};
 }
 
-// The scene-specialised kernels keep the default strategy: under max-ilp scene 0 and 4K ran level, Cornell -5 % on one
-// box and level on another, Perlin +23 % (profiles/r05_ab_s54_*, r05_ab_s56_*, r05_ab_s57_*).  RT_STATIC_SCHED=<strategy>
-// (A/B) builds them with another.
-std::vector<std::string> static_sched(const SceneImage &) { return sched_options("RT_STATIC_SCHED", false); }
+// The scene-specialised kernels: max-ilp except with noise textures.  Built by LLVM 22 (round 6) with loops unrolled
+// only where asked, max-ilp took scene 0 from 32.1-32.8 to 31.6-31.9 ms and Cornell from 214-216 to 208-211, while the
+// Perlin kernel ran +20 % (99 -> 119-121 ms) (profiles/r06_ab_unroll_*.jsonl; round 5 under LLVM 20: scene 0 level,
+// Cornell -5 % on one box, Perlin +23 %).  RT_STATIC_SCHED=<strategy> (A/B) builds them with another.
+std::vector<std::string> static_sched(const SceneImage &img) { return sched_options("RT_STATIC_SCHED", !img.has_noise); }
 
 bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool fold, JitKernels *out, std::string *why) {
   std::string src;

@@ -115,6 +115,9 @@ int rt_write_ppm(const char *path, const float *rgb, uint32_t width, uint32_t he
 /* sizes of the ABI structs as compiled (bindings check their mirrors against these):
  * [rt_scene, rt_camera, rt_params, rt_stats, rt_settings, rtr_hittable, rtr_material, rtr_texture] */
 int rt_abi_struct_sizes(uint32_t *out, int n);
+/* Build stamp of this library (see rt_hip_build_hash in rt_render.h) */
+const char *rt_host_build_hash(void);
+const char *rt_host_build_files(void);
 
 #ifdef __cplusplus
 }

@@ -36,6 +36,8 @@ extern "C" {
 #define RT_ERR_NO_DEVICE     -4   /* no HIP device visible */
 #define RT_ERR_STACK         -5   /* scene needs a deeper traversal stack than the kernel supports */
 #define RT_ERR_UNSUPPORTED   -6   /* feature outside this build */
+#define RT_ERR_DEVICE_CHECK  -7   /* a kernel built with device checks (RT_CHECKS=1) found an index out of its capacity;
+                                     rt_context_note names the site, the index and the capacity (rt_context_timing) */
 
 /* Scene bytes exactly as the reference builds them (raytracing.cu:1699-1733). */
 typedef struct rt_scene {
@@ -126,8 +128,8 @@ typedef struct rt_kernel_info {
   int32_t blocks_per_cu;   /* resident blocks per CU the launch used (0 if not launched) */
   int32_t run_time;        /* 1: run-time compiled (hipRTC), 0: an offline kernel of librt_hip.so */
   char compiler[128];      /* the compiler's identification ("AMD clang version ..."), "" if unknown */
-  char loader[128];        /* run-time kernels: where their hipRTC came from ("dlmopen:/opt/rocm/lib/libhiprtc.so.7" or
-                              "process"); offline kernels: "" */
+  char loader[128];        /* run-time kernels: where they were compiled ("helper:<lib dir>/rt_jitc", the child process
+                              linked against /opt/rocm's hipRTC, or "process": this process's hipRTC); offline kernels: "" */
 } rt_kernel_info;
 
 typedef struct rt_stats {
@@ -293,6 +295,10 @@ int rt_rng_table_states(uint64_t seed, int width, int row_offset, int row_stride
 const char *rt_context_note(const rt_context *ctx);
 
 const char *rt_status_string(int status);
+/* Build stamp: the files this library was built from (space separated, repository-relative) and the first 16 hex digits
+ * of the sha256 of their bytes in that order; the Python binding refuses a library that does not match its tree. */
+const char *rt_hip_build_hash(void);
+const char *rt_hip_build_files(void);
 int rt_device_count(int *count);
 int rt_abi_version(void);
 

@@ -61,3 +61,21 @@ def test_product_path_never_loads_oracle():
     for f in srcs:
         t = f.read_text()
         assert "rt_render_cpu" not in t and "liboracle" not in t and "oracle_lib" not in t, f
+
+
+def test_build_stamp_refuses_a_stale_library(tmp_path, monkeypatch):
+    # the libraries record the sources they were built from; a tree whose sources differ is refused loudly
+    lib = C.CDLL(str(_abi.HIP_LIB))
+    _abi.check_build_stamp(lib, "rt_hip", _abi.HIP_LIB)        # this tree: accepted
+    lib.rt_hip_build_files.restype = C.c_char_p
+    files = lib.rt_hip_build_files().decode().split()
+    assert "cuda_raytracing_amd/csrc/device/rt_body.h" in files and "cuda_raytracing_amd/csrc/rt_capi.cpp" in files
+    for name in files:
+        dst = tmp_path / name
+        dst.parent.mkdir(parents=True, exist_ok=True)
+        dst.write_bytes((REPO / name).read_bytes())
+    (tmp_path / "cuda_raytracing_amd/csrc/device/rt_body.h").write_bytes(
+        (REPO / "cuda_raytracing_amd/csrc/device/rt_body.h").read_bytes() + b"// edited after the build\n")
+    monkeypatch.setattr(_abi, "REPO_DIR", tmp_path)
+    with pytest.raises(RuntimeError, match="stale library"):
+        _abi.check_build_stamp(lib, "rt_hip", _abi.HIP_LIB)

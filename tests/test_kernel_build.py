@@ -1,0 +1,40 @@
+"""The run-time render kernels of every BASELINE config, built here by the run-time compiler (no device): no register
+spilled to scratch, and the compiler is ROCm 7.2's hipRTC (AMD clang 22) in rt_jitc, a child process linked against
+/opt/rocm, although torch is imported first in this process and its bundled ROCm 7.0 hipRTC (LLVM 20, which miscompiled
+the verified sphere walk: DESIGN §2) is what the process itself resolves.  rt_kernel_build applies the same source,
+options and register-budget rules as a render (before the device-dependent residency step, which itself keeps a build
+only without scratch)."""
+from __future__ import annotations
+
+import pytest
+
+import torch  # noqa: F401  first, as in every test / bench process: its ROCm 7.0 hipRTC is what the process resolves
+
+import cuda_raytracing_amd as rt
+
+# (scene, traversal, max_bounces) of BASELINE configs 2-5 (config 1 is config 2's kernel at d4 on the CPU path)
+CONFIG_KERNELS = [
+    (0, rt.RT_TRAV_STATIC, 16),    # config 2: scene 0, d16
+    (1, rt.RT_TRAV_STATIC, 50),    # config 3 as indexed: Cornell, d50
+    (17, rt.RT_TRAV_STATIC, 50),   # config 3 as named: Perlin, d50
+    (20, rt.RT_TRAV_ACCEL, 16),    # config 4: 10k spheres, d16 (verified sphere walk at its 6-wave budget)
+    (0, rt.RT_TRAV_STATIC, 50),    # config 5: scene 0, d50
+]
+
+
+@pytest.mark.parametrize("scene,trav,mb", CONFIG_KERNELS)
+def test_baseline_config_kernels_build_without_spills(scene, trav, mb):
+    w, _ = rt.build_scene(scene)
+    k = rt.kernel_build(w.scene(), trav, mb)
+    assert k["run_time"] == 1
+    assert k["scratch_bytes"] == 0, k
+    assert k["vgpr_spills"] == 0, k
+    assert 0 < k["vgprs"] <= 128 and k["agprs"] == 0, k
+    assert "clang version 22" in k["compiler"], k
+    assert k["loader"].startswith("helper:"), k
+
+
+def test_final_scene_mixed_walk_builds_without_spills():
+    w, _ = rt.build_scene(3)
+    k = rt.kernel_build(w.scene(), rt.RT_TRAV_MIXED, 40)
+    assert k["scratch_bytes"] == 0 and k["vgpr_spills"] == 0, k
