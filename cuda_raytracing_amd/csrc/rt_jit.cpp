@@ -270,7 +270,9 @@ bool jit_source(const SceneImage &img, int variant, uint32_t max_visits, bool fo
 // The on-disk cache key hashes this whole vector (build_module): bit-exact parity rests on these flags.
 std::vector<std::string> jit_options(const std::string &arch, const std::vector<std::string> &extra) {
   std::vector<std::string> o = {"--offload-arch=" + arch, "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                                "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"};
+                                "-fhip-fp32-correctly-rounded-divide-sqrt"};
+  // RT_JIT_SLP=1 (A/B): let the SLP vectoriser pack f32 pairs into v_pk_* (off by default, above)
+  if (const char *e = std::getenv("RT_JIT_SLP"); !(e && e[0] == '1')) o.push_back("-fno-slp-vectorize");
   // Loops are unrolled only where the source asks (#pragma unroll): ROCm 7.2's LLVM 22 otherwise also unrolls the
   // colour-stack unwind and the rejection loops of the scene-specialised kernels (+11 % static VALU instructions, scene 0
   // render +4 % against the LLVM 20 build; without: level, profiles/r06_ab_unroll_*.jsonl).  RT_JIT_UNROLL=1 (A/B)
