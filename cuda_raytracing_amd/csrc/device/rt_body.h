@@ -86,9 +86,13 @@ struct Mem {
 // and the caller skips the access.  Without RT_DEVICE_CHECKS it is the constant true and compiles away.
 // ---------------------------------------------------------------------------------------------
 __device__ __noinline__ bool check_fail(const RenderArgs &A, uint32_t site, uint32_t index, uint32_t cap) {
-  if (atomicCAS(A.work + kCheckWord, 0u, site) == 0u) {
-    atomicExch(A.work + kCheckWord + 1, index);
-    atomicExch(A.work + kCheckWord + 2, cap);
+  // the address and the values through VGPRs: with wave-uniform operands the instruction selector may otherwise pick a
+  // scalar-memory atomic (LLVM 22 did, and then failed to encode it for gfx950); these are vector (global) atomics
+  uint32_t *w = A.work + kCheckWord;
+  asm volatile("" : "+v"(w), "+v"(site), "+v"(index), "+v"(cap));
+  if (atomicCAS(w, 0u, site) == 0u) {
+    atomicExch(w + 1, index);
+    atomicExch(w + 2, cap);
   }
   return false;
 }

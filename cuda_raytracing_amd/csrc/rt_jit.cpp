@@ -84,7 +84,7 @@ std::string helper_path() {
   return "rt_jitc";
 }
 
-// run the helper with `args`; its exit status (-1: it could not be started)
+// run the helper with `args`; its exit status (-1: it could not be started, -2 - n: killed by signal n)
 int run_helper(const std::string &exe, const std::vector<std::string> &args, const std::string &out_file = "") {
   std::vector<char *> argv;
   argv.push_back(const_cast<char *>(exe.c_str()));
@@ -100,7 +100,7 @@ int run_helper(const std::string &exe, const std::vector<std::string> &args, con
   int status = 0;
   while (waitpid(pid, &status, 0) < 0)
     if (errno != EINTR) return -1;
-  return WIFEXITED(status) ? WEXITSTATUS(status) : -1;
+  return WIFEXITED(status) ? WEXITSTATUS(status) : WIFSIGNALED(status) ? -2 - WTERMSIG(status) : -1;
 }
 
 bool write_file(const std::string &p, const std::string &data) {
@@ -203,7 +203,10 @@ bool compile_in_helper(const std::string &exe, const std::string &src, const std
   std::string lg, co;
   read_file(dir + "/log.txt", &lg);
   ok = rc == 0 && read_file(dir + "/code.co", &co) && !co.empty();
-  if (log) *log = rc < 0 ? "the kernel compiler " + exe + " could not be started" : lg;
+  if (log)
+    *log = rc == -1 ? "the kernel compiler " + exe + " could not be started"
+         : rc < -1  ? "the kernel compiler " + exe + " died of signal " + std::to_string(-2 - rc) + ": " + lg
+                    : lg;
   if (ok) code->assign(co.begin(), co.end());
   for (const char *f : files) std::remove((dir + f).c_str());
   rmdir(dir.c_str());

@@ -6,6 +6,9 @@ options and register-budget rules as a render (before the device-dependent resid
 only without scratch)."""
 from __future__ import annotations
 
+import re
+from pathlib import Path
+
 import pytest
 
 import torch  # noqa: F401  first, as in every test / bench process: its ROCm 7.0 hipRTC is what the process resolves
@@ -38,3 +41,34 @@ def test_final_scene_mixed_walk_builds_without_spills():
     w, _ = rt.build_scene(3)
     k = rt.kernel_build(w.scene(), rt.RT_TRAV_MIXED, 40)
     assert k["scratch_bytes"] == 0 and k["vgpr_spills"] == 0, k
+
+
+def _render_kernel_isa(tmp_path, monkeypatch, scene, trav, mb, **env):
+    """Disassembly of the render kernel rt_kernel_build compiles (RT_JIT_DUMP keeps its code object)."""
+    import shutil
+    import subprocess
+    objdump = shutil.which("llvm-objdump") or "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not Path(objdump).exists():
+        pytest.skip("llvm-objdump not available")
+    d = tmp_path / f"dump_{scene}_{trav}_{mb}"
+    d.mkdir()
+    monkeypatch.setenv("RT_JIT_DUMP", str(d))
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    w, _ = rt.build_scene(scene)
+    rt.kernel_build(w.scene(), trav, mb)
+    cos = list(d.glob("*.co"))
+    assert cos, "no code object dumped"
+    return "".join(subprocess.run([objdump, "-d", "--mcpu=gfx950", str(c)], capture_output=True, text=True,
+                                  check=True).stdout for c in cos)
+
+
+@pytest.mark.parametrize("scene,trav,mb,checks", [(0, rt.RT_TRAV_STATIC, 16, "0"), (20, rt.RT_TRAV_ACCEL, 16, "0"),
+                                                  (17, rt.RT_TRAV_STATIC, 50, "0"), (3, rt.RT_TRAV_MIXED, 40, "0"),
+                                                  (0, rt.RT_TRAV_LANE, 8, "1"), (20, rt.RT_TRAV_ACCEL, 16, "1")])
+def test_kernels_write_memory_through_vector_instructions_only(tmp_path, monkeypatch, scene, trav, mb, checks):
+    # no scalar-cache writes (s_store / s_atomic / s_dcache_wb) in any render kernel, device-checked builds included
+    # (their check routine's atomics are forced into VGPR operands: with uniform operands LLVM 22 selected a scalar atomic)
+    isa = _render_kernel_isa(tmp_path, monkeypatch, scene, trav, mb, RT_CHECKS=checks)
+    bad = [ln for ln in isa.splitlines() if re.search(r"\bs_(store|atomic|buffer_store|buffer_atomic|dcache_wb|scratch_store)", ln)]
+    assert not bad, bad[:5]
