@@ -540,6 +540,8 @@ def main():
                         + (" + gather to rank 0" if world_size > 1 else ""),
                 "pixels_per_gpu": rows * W,
                 "traversal": TRAV_NAMES.get(cst.traversal, str(cst.traversal)),
+                # the launched render kernel as the register allocator built it (rt_stats.kernel, code-object metadata)
+                "kernel_build": fstats[-1].kernel.as_dict(),
                 "kernel": {rt.RT_TRAV_STATIC: "rt_static_render (hipRTC)", rt.RT_TRAV_ACCEL: "rt_accel_render (hipRTC)",
                            rt.RT_TRAV_MIXED: "rt_mixed_render (hipRTC)"}.get(
                     cst.traversal, "rt_lane_render (hipRTC)"),
