@@ -2677,9 +2677,15 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           const uint32_t k = ((plr & ((1u << tsh) - 1u)) << ts) | (pj & twm);
           float *o = A.out + static_cast<size_t>(tile) * 192u + 3u * k;
           if (RT_CHECK(A, tile * 64u + k < A.n_ids, CHK_PIXEL, tile * 64u + k, A.n_ids)) {
+#ifdef RT_NT_FRAME   // A/B (RT_JIT_OPTS=-DRT_NT_FRAME): non-temporal stores of the tile frame
+            __builtin_nontemporal_store(c.x, &o[0]);
+            __builtin_nontemporal_store(c.y, &o[1]);
+            __builtin_nontemporal_store(c.z, &o[2]);
+#else
             o[0] = c.x;
             o[1] = c.y;
             o[2] = c.z;
+#endif
           }
         } else if (RT_CHECK(A, plr < A.rows && pj < static_cast<uint32_t>(A.width), CHK_PIXEL, pxy, (A.rows << 16) | A.width)) {
           const size_t pix = static_cast<size_t>(plr) * static_cast<uint32_t>(A.width) + pj;
