@@ -328,7 +328,7 @@ struct rt_context {
   int stage_slots = 0;             // (stage_slots_setting; -1: compiled in, none at launch)
   uint32_t used_stage_slots = 0;   // the last render's
   int tiled_out = -1;              // 1: the render writes the frame tile-major, untile_kernel the rows + bytes; 0: row-major
-                                   // stores; -1 (default): tile-major unless the scene has noise textures (RT_TILED_OUT)
+                                   // stores; -1 (default): tile-major (RT_TILED_OUT)
   bool used_tiled = false;         // the last render's
   int tail_chunk = 0;              // RT_TAIL_CHUNK: the tail of the order in pieces of this many pixels (0: whole tiles)
   double tail_gen = 1.0;           // RT_TAIL_GEN: ... over this many times the grid's lanes of ids
@@ -778,11 +778,10 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
                                (c->lds ? static_cast<size_t>(scene_lds_words) * 4 : 4096u /* staged SAH top nodes */) +
                                (stackless ? kRngSlotBytes : full_stack_bytes) + kLdsReserve;
   const bool rc_lds_only = c->rc_lds_auto && !c->rc_lds_only_off && lds_only_need <= kLdsPerCu / kRcLdsOnlyBlocks;
-  // tile-major output (run-time kernels; not with output staging, which stores whole tiles row-major itself).  By
-  // default not in kernels with noise textures: there the same store made the Perlin d50 kernel 15-21 % slower at the
-  // same registers and LDS (code generation; scene 0, Cornell and 10k within 0-1 %)
-  const bool tiled_kernel = (c->tiled_out == 1 || (c->tiled_out < 0 && !c->img.has_noise)) && c->stage_slots == 0 &&
-                            out_dev != nullptr;
+  // tile-major output (run-time kernels; not with output staging, which stores whole tiles row-major itself), in every
+  // kernel since round 6: the Perlin d50 kernel's 15-21 % slowdown with it (round 5) was the LLVM 20 build's;
+  // built by LLVM 22 it runs level (profiles/r06_ab_perlin_tiled.jsonl: 98.8 / 98.7 / 97.7 vs 99.3 / 98.9 / 99.3 ms)
+  const bool tiled_kernel = c->tiled_out != 0 && c->stage_slots == 0 && out_dev != nullptr;
   // the deep-level pool's code in run-time kernels with HBM levels (sized below, once the residency is known)
   // (by default deep kernels with automatic levels; pinned levels, RT_RC_LDS_LEVELS, get one only with RT_RC_POOL)
   const bool pool_kernel = c->rc_pool > 0 && !rc_lds_only &&
@@ -1516,10 +1515,10 @@ static int kernel_source_impl(const rt_scene *scene, int traversal, int32_t max_
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 65536u ? rt::kVarNarrow : 0) |
                       (!img.has_noise && !img.needs_uv && img.rec_consts + rt::kRcConsts < 255u ? rt::kVarByte : 0) |
                       static_cast<int>(tile_shift_setting() << rt::kVarTileShift) | (stage_slots_setting() ? rt::kVarStage : 0);
-  {   // tile-major output as a render with a device frame decides (RT_TILED_OUT, noise textures, output staging)
+  {   // tile-major output as a render with a device frame decides (RT_TILED_OUT, output staging)
     const char *e = std::getenv("RT_TILED_OUT");
     const int t = e ? (e[0] == '1' ? 1 : (e[0] == '0' ? 0 : -1)) : -1;
-    if ((t == 1 || (t < 0 && !img.has_noise)) && !stage_slots_setting()) variant |= rt::kVarTiledOut;
+    if (t != 0 && !stage_slots_setting()) variant |= rt::kVarTiledOut;
   }
   {   // kVarRcLds as a static-traversal render would set it (scene in LDS, no per-lane stacks), else the pool's code
     const uint32_t cb = (variant & rt::kVarByte) ? 1u : ((variant & rt::kVarNarrow) ? 2u : 4u);

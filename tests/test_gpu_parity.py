@@ -496,8 +496,8 @@ def test_fused_ppm_bytes_match_host_tonemap(idx, W, H, spp, b):
 @pytest.mark.parametrize("idx,W,H,spp,b", [(0, 96, 54, 8, 16), (17, 64, 36, 4, 50), (1, 40, 40, 4, 50), (20, 72, 44, 2, 8),
                                            (3, 40, 40, 2, 8), (0, 33, 7, 2, 16), (0, 260, 20, 1, 4)])
 def test_tiled_output_matches_oracle(idx, W, H, spp, b, tile_w, tiled, monkeypatch):
-    # Tile-major output (the default without noise textures; RT_TILED_OUT=0: each pixel stored row-major with its bytes
-    # by the render kernel, =1: tile-major in every kernel):
+    # Tile-major output (the default, since round 6 with noise textures too; RT_TILED_OUT=0: each pixel stored row-major
+    # with its bytes by the render kernel, =1: tile-major):
     # the render kernel writes the float frame tile-major and untile_kernel writes the caller's row-major floats and
     # the P6 bytes in 128-column bands — bit-identical to the oracle and to the host tonemap, partial edge tiles and
     # bands included, on the static (LDS-only and pooled deep kernels), verified sphere and mixed walks, 8x8 and 32x2
@@ -521,8 +521,7 @@ def test_tiled_output_matches_oracle(idx, W, H, spp, b, tile_w, tiled, monkeypat
     assert np.array_equal(out8.cpu().numpy(), rt.tonemap(ref))
     fb2, st = gpu(w.scene(), cam, p)   # the one-shot entry point (host copy of the floats)
     assert np.array_equal(bits(fb2), bits(ref))
-    noise = idx in (3, 17)   # final_scene's marble sphere, perlin_spheres
-    assert st.tiled_out == (1 if tiled == "1" or (tiled == "auto" and not noise) else 0)
+    assert st.tiled_out == (0 if tiled == "0" else 1)   # tile-major by default, noise scenes included (round 6)
 
 
 def _random_world(seed: int):

@@ -61,11 +61,12 @@ def test_kernel_variants_deep_pool_and_lds_only(monkeypatch):
 
 
 def test_kernel_variants_opt_in_paths(monkeypatch):
-    # tile-major output by default without noise textures (RT_TILED_OUT=0/1 and output staging decide otherwise); no
-    # tail-piece code unless asked
+    # tile-major output by default, noise textures included since round 6 (RT_TILED_OUT=0 and output staging decide
+    # otherwise); no tail-piece code unless asked
     v = _variant_of(0, rt.RT_TRAV_STATIC, 16, monkeypatch)
     assert v & K_VAR_TILED and not v & K_VAR_TAIL
-    assert not _variant_of(17, rt.RT_TRAV_STATIC, 50, monkeypatch) & K_VAR_TILED
+    assert _variant_of(17, rt.RT_TRAV_STATIC, 50, monkeypatch) & K_VAR_TILED
+    assert not _variant_of(17, rt.RT_TRAV_STATIC, 50, monkeypatch, RT_TILED_OUT="0") & K_VAR_TILED
     assert _variant_of(17, rt.RT_TRAV_STATIC, 50, monkeypatch, RT_TILED_OUT="1") & K_VAR_TILED
     assert not _variant_of(0, rt.RT_TRAV_STATIC, 16, monkeypatch, RT_TILED_OUT="0") & K_VAR_TILED
     assert not _variant_of(0, rt.RT_TRAV_STATIC, 16, monkeypatch, RT_STAGE_SLOTS="4") & K_VAR_TILED
