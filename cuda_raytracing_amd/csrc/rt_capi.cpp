@@ -266,12 +266,6 @@ struct rt_context {
   PinBuf rows_stage, cols_stage;   // their pinned staging (stream-ordered uploads)
   bool ev_recorded = false;        // ev[2] has been recorded (a frame was enqueued before)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};   // seed | schedule (probe + order) | render
-  // Tile-major frames: untile_kernel runs on a high-priority stream of its own (between the render's end and the frame's
-  // end event on the caller's stream), so that with frames in flight its blocks are dispatched ahead of the next frame's
-  // persistent render blocks instead of waiting behind them (round 5: 10.1 ms average, 26 ms worst, for a 13-us kernel).
-  // RT_UNTILE_PRIO=0 (A/B) launches it on the caller's stream.
-  hipStream_t untile_stream = nullptr;
-  hipEvent_t ev_untile[2] = {nullptr, nullptr};   // render done (caller's stream) | untile done (untile_stream)
   bool lds = false;
   bool counted = false;
   int variant = 0;
@@ -498,8 +492,6 @@ void rt_context_destroy(rt_context *c) {
   {
     DeviceGuard g(c->device);
     for (hipEvent_t &e : c->ev) if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t &e : c->ev_untile) if (e) (void)hipEventDestroy(e);
-    if (c->untile_stream) (void)hipStreamDestroy(c->untile_stream);
     c->scene.release(); c->jump.release(); c->rng_rows.release(); c->rng_cols.release(); c->prim_lists.release(); c->prim_counts.release(); c->rc.release();
     c->work.release(); c->counters.release();
     c->wave_trace.release(); c->tile_cost.release(); c->tile_order.release(); c->tiled.release();
@@ -624,12 +616,6 @@ int rt_context_create(const rt_scene *scene, int device, rt_context **out) {
            
             c->counters.ensure(RT_CNT__COUNT * sizeof(unsigned long long)) == hipSuccess;
   for (hipEvent_t &e : c->ev) ok = ok && hipEventCreate(&e) == hipSuccess;
-  if (const char *e = std::getenv("RT_UNTILE_PRIO"); !(e && e[0] == '0')) {
-    int least = 0, greatest = 0;
-    ok = ok && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
-         hipStreamCreateWithPriority(&c->untile_stream, hipStreamNonBlocking, greatest) == hipSuccess;
-    for (hipEvent_t &ev : c->ev_untile) ok = ok && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
-  }
   if (!ok) { rt_context_destroy(c); return RT_ERR_HIP; }
   *out = c;
   return RT_OK;
@@ -1294,18 +1280,9 @@ int rt_context_render_ppm(rt_context *c, const rt_camera *cam, const rt_params *
   const hipError_t le = jit_fn ? rt::jit_launch(jit_fn, a, static_cast<uint32_t>(blocks), c->lds_bytes, s)
                                : rt::launch_render(a, c->variant, static_cast<uint32_t>(blocks), c->lds_bytes, s);
   if (le != hipSuccess) return RT_ERR_HIP;
-  if (tiled) {
-    hipStream_t us = c->untile_stream ? c->untile_stream : s;
-    if (c->untile_stream &&
-        (hipEventRecord(c->ev_untile[0], s) != hipSuccess || hipStreamWaitEvent(us, c->ev_untile[0], 0) != hipSuccess))
-      return RT_ERR_HIP;
-    if (rt::launch_untile(static_cast<const float *>(c->tiled.p), out_dev, out8_dev, static_cast<uint32_t>(p->row_count),
-                          static_cast<uint32_t>(p->width), tiles_x, tile_shift, us) != hipSuccess)
-      return RT_ERR_HIP;
-    if (c->untile_stream &&
-        (hipEventRecord(c->ev_untile[1], us) != hipSuccess || hipStreamWaitEvent(s, c->ev_untile[1], 0) != hipSuccess))
-      return RT_ERR_HIP;
-  }
+  if (tiled && rt::launch_untile(static_cast<const float *>(c->tiled.p), out_dev, out8_dev, static_cast<uint32_t>(p->row_count),
+                                 static_cast<uint32_t>(p->width), tiles_x, tile_shift, s) != hipSuccess)
+    return RT_ERR_HIP;
   if (hipEventRecord(c->ev[2], s) != hipSuccess) return RT_ERR_HIP;
   c->ev_recorded = true;
   c->last_cam = *cam;

@@ -192,11 +192,6 @@ constexpr uint32_t kUntileCols = 128;
 __global__ __launch_bounds__(256) void untile_kernel(const float *__restrict__ tiled, float *__restrict__ out,
                                                      uint8_t *__restrict__ out8, uint32_t rows, uint32_t width,
                                                      uint32_t tiles_x, uint32_t ts) {
-  // top issue priority: with frames in flight this kernel shares the SIMDs with the next frame's render waves, whose
-  // costliest-tile and tail waves run at s_setprio 2-3 and otherwise win every issue arbitration (round 5: 13 us alone,
-  // 10 ms average / 26 ms worst behind a render kernel; the high-priority stream alone did not change that: it orders
-  // dispatch, not issue)
-  __builtin_amdgcn_s_setprio(3);
   const uint32_t tsh = 6u - ts, th = 1u << tsh, x0 = blockIdx.x * kUntileCols, y0 = blockIdx.y * th;
   for (uint32_t idx = threadIdx.x; idx < th * kUntileCols * 3u; idx += 256u) {
     const uint32_t r = idx / (kUntileCols * 3u), f = idx - r * (kUntileCols * 3u);
