@@ -86,7 +86,7 @@ class World:
 
     def image(self, name: str = "earthmap.jpg") -> _abi.Material:
         """Image texture from a file (stbi_loadf semantics, load_image); a missing or undecodable file
-        renders magenta like the reference's failed load; GIF / PSD / PIC make status() RT_ERR_UNSUPPORTED."""
+        renders magenta like the reference's failed load."""
         return self._L.rt_mat_lambert_image(self._w, name.encode())
 
     def status(self) -> int:
@@ -213,9 +213,9 @@ def build_scene(index: int, capacity: int | None = None):
 
 def load_image(path: str):
     """rt_image_load: float32 [H, W, 3] texels as stbi_loadf(path, .., 3) returns them (row 0 = top; JPEG,
-    PNG, BMP, TGA, PNM with 8-bit channels as powf(c/255, 2.2); Radiance HDR as stored), or None when the
-    file does not exist or stb would fail to load it (the reference's failed load: a magenta texture).
-    RenderError(RT_ERR_UNSUPPORTED) for GIF / PSD / PIC files, which this build does not decode."""
+    PNG, BMP, TGA, GIF, PSD, Softimage PIC, PNM with 8-bit channels as powf(c/255, 2.2); Radiance HDR as
+    stored), or None when the file does not exist or stb would fail to load it (the reference's failed load:
+    a magenta texture)."""
     L = _abi.host_lib()
     p = C.POINTER(C.c_float)()
     w, h = C.c_int32(0), C.c_int32(0)

@@ -9,13 +9,14 @@
 //   - its FILE reader (stbi__start_file :877 and the context functions :1597-1689): a 128-byte buffer
 //     refilled by fread, zeros once the file is exhausted, "rewind" back to the first buffer after each
 //     format test, skips by fseek — so truncated and odd files read the same bytes as they do there;
-//   - the BMP (:5346-5732), TGA (:5739-6074), PNM (:7494-7629) and HDR (:7087-7287) decoders;
-//     JPEG and PNG are image_jpeg.cpp and image_png.cpp.
-// A file stb would decode as GIF, PSD or Softimage PIC is RT_ERR_UNSUPPORTED (those decoders are not
-// restated).  A file that does not exist, is of no known type or fails to decode is the reference's
-// failed load, RT_IMAGE_MISSING: no pixels, the texture renders magenta (:346-347).  One deliberate
-// difference: where stb "succeeds" with a zero-area image (a BMP or HDR header saying width 0), the
-// reference's texel lookup would index outside the buffer; such a file is RT_IMAGE_MISSING here.
+//   - the BMP (:5346-5732), TGA (:5739-6074), PSD (:6081-6325), Softimage PIC (:6336-6546), GIF (:6553-7081,
+//     the first image), PNM (:7494-7629) and HDR (:7087-7287) decoders; JPEG and PNG are image_jpeg.cpp and
+//     image_png.cpp.
+// A file that does not exist, is of no known type or fails to decode is the reference's failed load,
+// RT_IMAGE_MISSING: no pixels, the texture renders magenta (:346-347).  Two deliberate differences: where stb
+// "succeeds" with a zero-area image (a BMP, HDR, GIF, PSD or PIC header saying width 0), the reference's texel
+// lookup would index outside the buffer; and where a corrupt PIC file of non-zero area fails stb's core loop, stb
+// converts the NULL it got back and faults.  Both are RT_IMAGE_MISSING here.
 // The BMP helpers high_bit / bitcount / shiftsigned are stb's (:5370-5413) with the same tables.
 //
 // Provenance and licence.  Parts of this file are DERIVED FROM stb_image v2.30 (Sean Barrett and contributors,
@@ -41,6 +42,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "image_decoders.h"
@@ -746,6 +748,374 @@ bool hdr_load(StbFile &s, std::vector<float> *data, int *pw, int *ph) {
   return true;
 }
 
+// ---- Photoshop PSD (:6126-6325, as stbi_loadf runs it: 8-bit output) ----
+// RGB colour mode only; 8- or 16-bit channels (a 16-bit raw sample keeps its high byte; RLE data is read as bytes
+// whatever the depth); channels past the file's are 0, alpha 255; a pixel with partial alpha loses the white matte.
+
+// PackBits into every 4th byte: n < 128 copies n + 1 bytes, n > 128 repeats the next byte 257 - n times, 128 is a
+// no-op; a run past the channel's end is corrupt (:6088-6124)
+bool psd_rle_channel(StbFile &s, uint8_t *p, int count) {
+  int done = 0;
+  while (count - done > 0) {
+    const int left = count - done;
+    int n = static_cast<int>(s.get8());
+    if (n == 128) continue;
+    if (n < 128) {
+      n += 1;
+      if (n > left) return false;
+      for (int i = 0; i < n; ++i, p += 4) *p = static_cast<uint8_t>(s.get8());
+    } else {
+      n = 257 - n;
+      if (n > left) return false;
+      const uint8_t v = static_cast<uint8_t>(s.get8());
+      for (int i = 0; i < n; ++i, p += 4) *p = v;
+    }
+    done += n;
+  }
+  return true;
+}
+
+bool psd_load(StbFile &s, Pixels *o) {
+  if (s.get32be() != 0x38425053u) return false;   // "8BPS"
+  if (s.get16be() != 1) return false;             // version
+  s.skip(6);
+  const int channels = s.get16be();
+  if (channels > 16) return false;
+  const int h = static_cast<int>(s.get32be()), w = static_cast<int>(s.get32be());   // as stb's int conversions
+  if (h > static_cast<int>(kMaxDim) || w > static_cast<int>(kMaxDim)) return false;
+  const int depth = s.get16be();
+  if (depth != 8 && depth != 16) return false;
+  if (s.get16be() != 3) return false;             // colour mode: RGB
+  for (int k = 0; k < 3; ++k) s.skip(static_cast<int>(s.get32be()));   // mode data, image resources, reserved
+  const int compression = s.get16be();
+  if (compression > 1) return false;
+  if (!mad3_ok(4, w, h, 0)) return false;
+  const int n = w * h;
+  o->px.assign(static_cast<size_t>(n) * 4, 0);
+  o->w = w;
+  o->h = h;
+  o->comp = 4;
+  uint8_t *out = o->px.data();
+  if (compression) s.skip(h * channels * 2);      // the per-row byte counts
+  for (int ch = 0; ch < 4; ++ch) {
+    uint8_t *p = out + ch;
+    if (ch >= channels) {
+      const uint8_t v = ch == 3 ? 255 : 0;
+      for (int i = 0; i < n; ++i) p[4 * i] = v;
+    } else if (compression) {
+      if (!psd_rle_channel(s, p, n)) return false;
+    } else if (depth == 16) {
+      for (int i = 0; i < n; ++i) p[4 * i] = static_cast<uint8_t>(s.get16be() >> 8);
+    } else {
+      for (int i = 0; i < n; ++i) p[4 * i] = static_cast<uint8_t>(s.get8());
+    }
+  }
+  if (channels >= 4) {   // un-premultiply against white: c / a + 255 (1 - 1 / a), in float, truncated to a byte
+    for (int i = 0; i < n; ++i) {
+      uint8_t *px = out + 4 * i;
+      if (px[3] == 0 || px[3] == 255) continue;
+      const float a = static_cast<float>(px[3]) / 255.0f;
+      const float ra = 1.0f / a;
+      const float inv_a = 255.0f * (1.0f - ra);
+      for (int c = 0; c < 3; ++c) {
+        const float v = static_cast<float>(px[c]) * ra + inv_a;
+        // (the C conversion of an out-of-range float to unsigned char, as the x86-64 build of stb executes it: to a
+        // 32-bit int, then its low byte; |v| < 2^17 here)
+        px[c] = static_cast<uint8_t>(static_cast<uint32_t>(static_cast<int32_t>(v)));
+      }
+    }
+  }
+  return true;
+}
+
+// ---- Softimage PIC (:6346-6539) ----
+// A 104-byte header (the 92 skipped bytes, width, height, ratio, fields, pad), a chain of at most 10 channel packets
+// (8 bits each; mask 0x80 R, 0x40 G, 0x20 B, 0x10 A), then per row, per packet: raw, pure-RLE or mixed-RLE runs of the
+// packet's channels.  Texels start at 255 in every channel.  (Where the data is corrupt and the picture has area, stb
+// converts the NULL it gets back from its core loop and faults; here that is a failed load.)
+struct PicPacket { uint8_t size, type, channel; };
+
+bool pic_value(StbFile &s, int channel, uint8_t *dest) {   // stbi__readval: an early end fails the read
+  for (int i = 0, mask = 0x80; i < 4; ++i, mask >>= 1) {
+    if (channel & mask) {
+      if (s.at_eof()) return false;
+      dest[i] = static_cast<uint8_t>(s.get8());
+    }
+  }
+  return true;
+}
+
+void pic_copy(int channel, uint8_t *dest, const uint8_t *src) {
+  for (int i = 0, mask = 0x80; i < 4; ++i, mask >>= 1)
+    if (channel & mask) dest[i] = src[i];
+}
+
+bool pic_load(StbFile &s, Pixels *o) {
+  for (int i = 0; i < 92; ++i) s.get8();
+  const int w = s.get16be(), h = s.get16be();
+  if (s.at_eof()) return false;
+  if (!mad3_ok(w, h, 4, 0)) return false;
+  s.get32be();   // ratio
+  s.get16be();   // fields
+  s.get16be();   // pad
+  o->px.assign(static_cast<size_t>(w) * h * 4, 0xff);
+  o->w = w;
+  o->h = h;
+  o->comp = 4;
+  PicPacket packets[10];
+  int count = 0;
+  uint32_t chained = 0;
+  do {
+    if (count == 10) return false;   // too many packets
+    PicPacket &p = packets[count++];
+    chained = s.get8();
+    p.size = static_cast<uint8_t>(s.get8());
+    p.type = static_cast<uint8_t>(s.get8());
+    p.channel = static_cast<uint8_t>(s.get8());
+    if (s.at_eof()) return false;
+    if (p.size != 8) return false;
+  } while (chained);
+  for (int y = 0; y < h; ++y) {
+    for (int k = 0; k < count; ++k) {
+      const PicPacket &p = packets[k];
+      uint8_t *dest = o->px.data() + static_cast<size_t>(y) * w * 4;
+      if (p.type == 0) {            // uncompressed
+        for (int x = 0; x < w; ++x, dest += 4)
+          if (!pic_value(s, p.channel, dest)) return false;
+      } else if (p.type == 1) {     // pure RLE: (count, value) pairs, a count past the row clamped to it
+        int left = w;
+        while (left > 0) {
+          int n = static_cast<int>(s.get8());
+          if (s.at_eof()) return false;
+          if (n > left) n = left;
+          uint8_t v[4];
+          if (!pic_value(s, p.channel, v)) return false;
+          for (int i = 0; i < n; ++i, dest += 4) pic_copy(p.channel, dest, v);
+          left -= n;
+        }
+      } else if (p.type == 2) {     // mixed RLE: >= 128 a repeat (128: 16-bit count follows), else count + 1 raw
+        int left = w;
+        while (left > 0) {
+          int n = static_cast<int>(s.get8());
+          if (s.at_eof()) return false;
+          if (n >= 128) {
+            n = n == 128 ? s.get16be() : n - 127;
+            if (n > left) return false;
+            uint8_t v[4];
+            if (!pic_value(s, p.channel, v)) return false;
+            for (int i = 0; i < n; ++i, dest += 4) pic_copy(p.channel, dest, v);
+          } else {
+            n += 1;
+            if (n > left) return false;
+            for (int i = 0; i < n; ++i, dest += 4)
+              if (!pic_value(s, p.channel, dest)) return false;
+          }
+          left -= n;
+        }
+      } else {
+        return false;               // unknown packet type
+      }
+    }
+  }
+  return true;
+}
+
+// ---- GIF (:6597-6950, 7048-7075): the first image of the file ----
+// The LZW raster (codes up to 12 bits, a clear code first), interlaced rows, global / local colour tables, the
+// graphic-control extension's transparent index (transparent texels are not written), and the first frame's
+// background: texels the image did not reach take the background entry of the global table when its index is not 0
+// — copied in the table's stored order (blue, green, red), as stb does.
+struct Gif {
+  int w = 0, h = 0, flags = 0, bgindex = 0, transparent = -1, eflags = 0, lflags = 0;
+  uint8_t pal[256][4] = {}, lpal[256][4] = {};
+  struct Code { int16_t prefix; uint8_t first, suffix; };
+  Code codes[8192] = {};
+  const uint8_t *table = nullptr;
+  int parse = 0, step = 0, start_x = 0, start_y = 0, max_x = 0, max_y = 0, cur_x = 0, cur_y = 0, line = 0;
+  std::vector<uint8_t> out, history;
+  std::vector<uint8_t> chain;   // a code's string, last texel first
+};
+
+void gif_table(StbFile &s, uint8_t pal[256][4], int n, int transp) {   // stored as blue, green, red, alpha
+  for (int i = 0; i < n; ++i) {
+    pal[i][2] = static_cast<uint8_t>(s.get8());
+    pal[i][1] = static_cast<uint8_t>(s.get8());
+    pal[i][0] = static_cast<uint8_t>(s.get8());
+    pal[i][3] = transp == i ? 0 : 255;
+  }
+}
+
+// the texels of one code, first to last (stbi__out_gif_code's recursion over the prefixes, unrolled): each one
+// written unless transparent, then the cursor moves on (interlace passes 8, 8 from 4, 4 from 2, 2 from 1)
+void gif_emit(Gif &g, int code) {
+  g.chain.clear();
+  for (int c = code; c >= 0; c = g.codes[c].prefix) g.chain.push_back(g.codes[c].suffix);
+  for (size_t k = g.chain.size(); k-- > 0;) {
+    if (g.cur_y >= g.max_y) continue;
+    const int idx = g.cur_x + g.cur_y;
+    uint8_t *p = &g.out[static_cast<size_t>(idx)];
+    g.history[static_cast<size_t>(idx / 4)] = 1;
+    const uint8_t *c = g.table + g.chain[k] * 4;
+    if (c[3] > 128) {
+      p[0] = c[2];
+      p[1] = c[1];
+      p[2] = c[0];
+      p[3] = c[3];
+    }
+    g.cur_x += 4;
+    if (g.cur_x >= g.max_x) {
+      g.cur_x = g.start_x;
+      g.cur_y += g.step;
+      while (g.cur_y >= g.max_y && g.parse > 0) {
+        g.step = (1 << g.parse) * g.line;
+        g.cur_y = g.start_y + (g.step >> 1);
+        --g.parse;
+      }
+    }
+  }
+}
+
+bool gif_raster(StbFile &s, Gif &g) {
+  const int lzw_cs = static_cast<int>(s.get8());
+  if (lzw_cs > 12) return false;
+  const int clear = 1 << lzw_cs;
+  bool first = true;   // a stream must open with a clear code
+  int codesize = lzw_cs + 1, codemask = (1 << codesize) - 1, bits = 0, valid_bits = 0;
+  for (int c = 0; c < clear; ++c) g.codes[c] = {-1, static_cast<uint8_t>(c), static_cast<uint8_t>(c)};
+  int avail = clear + 2, oldcode = -1, len = 0;
+  for (;;) {
+    if (valid_bits < codesize) {
+      if (len == 0) {
+        len = static_cast<int>(s.get8());   // the next data sub-block; an empty one ends the raster
+        if (len == 0) return true;
+      }
+      --len;
+      bits |= static_cast<int>(s.get8()) << valid_bits;
+      valid_bits += 8;
+      continue;
+    }
+    const int code = bits & codemask;
+    bits >>= codesize;
+    valid_bits -= codesize;
+    if (code == clear) {
+      codesize = lzw_cs + 1;
+      codemask = (1 << codesize) - 1;
+      avail = clear + 2;
+      oldcode = -1;
+      first = false;
+    } else if (code == clear + 1) {   // end of information: skip the rest of the sub-blocks
+      s.skip(len);
+      while ((len = static_cast<int>(s.get8())) > 0) s.skip(len);
+      return true;
+    } else if (code <= avail) {
+      if (first) return false;
+      if (oldcode >= 0) {
+        Gif::Code &p = g.codes[avail++];
+        if (avail > 8192) return false;
+        p.prefix = static_cast<int16_t>(oldcode);
+        p.first = g.codes[oldcode].first;
+        p.suffix = code == avail ? p.first : g.codes[code].first;
+      } else if (code == avail) {
+        return false;
+      }
+      gif_emit(g, code);
+      if ((avail & codemask) == 0 && avail <= 0x0fff) {
+        ++codesize;
+        codemask = (1 << codesize) - 1;
+      }
+      oldcode = code;
+    } else {
+      return false;
+    }
+  }
+}
+
+bool gif_load(StbFile &s, Pixels *o) {
+  std::unique_ptr<Gif> gp(new Gif());
+  Gif &g = *gp;
+  if (s.get8() != 'G' || s.get8() != 'I' || s.get8() != 'F' || s.get8() != '8') return false;
+  const uint32_t version = s.get8();
+  if (version != '7' && version != '9') return false;
+  if (s.get8() != 'a') return false;
+  g.w = s.get16le();
+  g.h = s.get16le();
+  g.flags = static_cast<int>(s.get8());
+  g.bgindex = static_cast<int>(s.get8());
+  s.get8();   // aspect ratio
+  if (g.flags & 0x80) gif_table(s, g.pal, 2 << (g.flags & 7), -1);
+  if (!mad3_ok(4, g.w, g.h, 0)) return false;
+  const size_t n = static_cast<size_t>(g.w) * g.h;
+  g.out.assign(4 * n, 0);
+  g.history.assign(n, 0);
+  for (;;) {
+    const uint32_t tag = s.get8();
+    if (tag == 0x2c) {   // image descriptor
+      const int x = s.get16le(), y = s.get16le(), w = s.get16le(), h = s.get16le();
+      if (x + w > g.w || y + h > g.h) return false;
+      g.line = g.w * 4;
+      g.start_x = x * 4;
+      g.start_y = y * g.line;
+      g.max_x = g.start_x + w * 4;
+      g.max_y = g.start_y + h * g.line;
+      g.cur_x = g.start_x;
+      g.cur_y = w == 0 ? g.max_y : g.start_y;
+      g.lflags = static_cast<int>(s.get8());
+      if (g.lflags & 0x40) {
+        g.step = 8 * g.line;
+        g.parse = 3;
+      } else {
+        g.step = g.line;
+        g.parse = 0;
+      }
+      if (g.lflags & 0x80) {
+        gif_table(s, g.lpal, 2 << (g.lflags & 7), (g.eflags & 0x01) ? g.transparent : -1);
+        g.table = &g.lpal[0][0];
+      } else if (g.flags & 0x80) {
+        g.table = &g.pal[0][0];
+      } else {
+        return false;   // no colour table
+      }
+      if (!gif_raster(s, g)) return false;
+      if (g.bgindex > 0) {
+        for (size_t i = 0; i < n; ++i) {
+          if (g.history[i] == 0) {
+            g.pal[g.bgindex][3] = 255;
+            std::memcpy(&g.out[4 * i], g.pal[g.bgindex], 4);
+          }
+        }
+      }
+      o->px.swap(g.out);
+      o->w = g.w;
+      o->h = g.h;
+      o->comp = 4;
+      return true;
+    }
+    if (tag == 0x21) {   // extension
+      int len;
+      if (s.get8() == 0xf9) {   // graphic control
+        len = static_cast<int>(s.get8());
+        if (len != 4) {
+          s.skip(len);
+          continue;
+        }
+        g.eflags = static_cast<int>(s.get8());
+        s.get16le();   // delay
+        if (g.transparent >= 0) g.pal[g.transparent][3] = 255;
+        if (g.eflags & 0x01) {
+          g.transparent = static_cast<int>(s.get8());
+          g.pal[g.transparent][3] = 0;
+        } else {
+          s.skip(1);
+          g.transparent = -1;
+        }
+      }
+      while ((len = static_cast<int>(s.get8())) != 0) s.skip(len);
+      continue;
+    }
+    return false;   // the trailer before any image, or an unknown block
+  }
+}
+
 bool read_file(const char *path, std::vector<uint8_t> *out) {
   FILE *f = std::fopen(path, "rb");
   if (!f) return false;
@@ -792,8 +1162,12 @@ int load(const std::vector<uint8_t> &bytes, float **rgb, int32_t *width, int32_t
     ok = rt::png::decode(bytes.data(), bytes.size(), &p.px, &p.w, &p.h);
   } else if (bmp_test(s)) {
     ok = bmp_load(s, &p);
-  } else if (gif_test(s) || psd_test(s) || pic_test(s)) {
-    return RT_ERR_UNSUPPORTED;
+  } else if (gif_test(s)) {
+    ok = gif_load(s, &p);
+  } else if (psd_test(s)) {
+    ok = psd_load(s, &p);
+  } else if (pic_test(s)) {
+    ok = pic_load(s, &p);
   } else if (jpeg_test(s)) {
     ok = rt::jpeg::decode(bytes.data(), bytes.size(), &p.px, &p.w, &p.h);
   } else if (pnm_test(s)) {

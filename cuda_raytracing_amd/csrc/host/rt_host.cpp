@@ -441,7 +441,7 @@ rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name) {
   // raytracing.cu:332-341 via stbi_loadf (image_load.cpp).  A missing or undecodable file is the
   // reference's failed load: pixels == NULL, width = height = 0, the texture renders magenta (:346-347) —
   // the catalog's earthmap.jpg is not in the reference repository, so that is what every reference run
-  // sees.  A GIF / PSD / PIC file (decoded by stb, not by this build) makes the world RT_ERR_UNSUPPORTED.
+  // sees.  (An RT_ERR_UNSUPPORTED from the loader, which no format stb decodes returns any more, is the world's status.)
   float *rgb = nullptr;
   int32_t width = 0, height = 0;
   const int st = rt_image_load(file_name, &rgb, &width, &height);

@@ -64,9 +64,8 @@ int32_t rt_world_rand(rt_world *w);
 rtr_material rt_mat_lambert_solid(rt_world *w, rtr_vec3 albedo);                 /* :1805 */
 rtr_material rt_mat_light_solid(rt_world *w, rtr_vec3 color);                    /* :1813 */
 /* :1821.  Loads the file like stbi_loadf(file, .., 3) (rt_image_load).  A missing, unknown or corrupt file
- * is the reference's failed load (magenta texture); a GIF / PSD / PIC file, which this build does not
- * decode, sets the world's status to RT_ERR_UNSUPPORTED (rt_world_status, returned by
- * rt_world_build_scene). */
+ * is the reference's failed load (magenta texture); should rt_image_load ever report RT_ERR_UNSUPPORTED,
+ * the world's status says so (rt_world_status, returned by rt_world_build_scene). */
 rtr_material rt_mat_lambert_image(rt_world *w, const char *file_name);
 /* an image texture whose load succeeded: width*height float RGB texels (stbi_loadf layout, row 0 first) */
 rtr_material rt_mat_lambert_image_pixels(rt_world *w, const float *rgb, int32_t width, int32_t height);
@@ -92,10 +91,10 @@ int rt_add_pyramid(rt_world *w, int xf, float angle, rtr_vec3 offset,
 
 /* ---- image files (make_image_texture's stbi_loadf, raytracing.cu:332-341) ----
  * *rgb = width*height float RGB texels, row 0 = top, as stb_image v2.30's stbi_loadf(path, .., 3) returns
- * them: JPEG (baseline + progressive), PNG, BMP, TGA, binary PNM with 8-bit channels as powf(c/255, 2.2),
- * Radiance HDR as stored; free with rt_image_free.  Returns RT_OK, RT_IMAGE_MISSING (no such file, or a
- * file stb would fail to load: the reference's failed load, a magenta texture) or RT_ERR_UNSUPPORTED (a
- * GIF, PSD or Softimage PIC file, which stb decodes and this build does not). */
+ * them: JPEG (baseline + progressive), PNG, BMP, TGA, GIF (first image), Photoshop PSD (RGB), Softimage
+ * PIC, binary PNM with 8-bit channels as powf(c/255, 2.2), Radiance HDR as stored; free with rt_image_free.
+ * Returns RT_OK or RT_IMAGE_MISSING (no such file, or a file stb would fail to load: the reference's failed
+ * load, a magenta texture). */
 #define RT_IMAGE_MISSING 1
 int rt_image_load(const char *path, float **rgb, int32_t *width, int32_t *height);
 void rt_image_free(float *rgb);

@@ -31,11 +31,43 @@ __attribute__((noinline)) static void rt_stbi_scrub_stack() {
 #define STB_IMAGE_IMPLEMENTATION
 #include "stb_image.h"
 
+#include <csetjmp>
+#include <csignal>
+
+// A corrupt Softimage PIC file of non-zero area makes stb convert the NULL its core loop returned (stbi__pic_load,
+// stb_image.h:6529-6536) and fault reading it.  The checker turns that fault into a reported crash
+// (rt_ref_stbi_crashed) instead of ending the test process: a segmentation fault inside the call jumps back here.
+static sigjmp_buf rt_stbi_jmp;
+static volatile sig_atomic_t rt_stbi_in_call = 0, rt_stbi_faulted = 0;
+static void rt_stbi_on_segv(int sig) {
+  if (rt_stbi_in_call) siglongjmp(rt_stbi_jmp, 1);
+  std::signal(sig, SIG_DFL);
+  std::raise(sig);
+}
+
 extern "C" float *rt_ref_stbi_loadf(const char *file, int *w, int *h) {
   int n = 0;
 #ifdef RT_STBI_FILL
   rt_stbi_scrub_stack();
 #endif
-  return stbi_loadf(file, w, h, &n, 3);   // make_image_texture's call: 3 channels
+  struct sigaction sa = {}, old_segv = {}, old_bus = {};
+  sa.sa_handler = rt_stbi_on_segv;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &old_segv);
+  sigaction(SIGBUS, &sa, &old_bus);
+  float *r = nullptr;
+  rt_stbi_faulted = 0;
+  if (sigsetjmp(rt_stbi_jmp, 1) == 0) {
+    rt_stbi_in_call = 1;
+    r = stbi_loadf(file, w, h, &n, 3);   // make_image_texture's call: 3 channels
+  } else {
+    rt_stbi_faulted = 1;
+    r = nullptr;
+  }
+  rt_stbi_in_call = 0;
+  sigaction(SIGSEGV, &old_segv, nullptr);
+  sigaction(SIGBUS, &old_bus, nullptr);
+  return r;
 }
+extern "C" int rt_ref_stbi_crashed() { return rt_stbi_faulted; }
 extern "C" void rt_ref_stbi_free(void *p) { stbi_image_free(p); }

@@ -3,7 +3,9 @@
 
 JPEG and most PNG / BMP / TGA files come from Pillow; the variants Pillow does not write (Adam7 PNG,
 chosen PNG filters and bit depths, DEFLATE block types, BMP bit-field / V4 / V5 / OS/2 headers, 16-bit
-and colour-mapped TGA, Radiance HDR) are encoded here from the format specifications.
+and colour-mapped TGA, Radiance HDR, GIF with chosen tables / interlace / transparency / clears, Photoshop PSD
+raw and RLE at 8 and 16 bits, Softimage PIC raw / pure / mixed RLE packets) are encoded here from the format
+specifications.
 """
 from __future__ import annotations
 
@@ -363,6 +365,234 @@ def hdr_expected(data_rgbe: np.ndarray) -> np.ndarray:
     return np.where(e == 0, np.float32(0), m * f).astype(np.float32)
 
 
+# ---------------------------------------------------------------- GIF (first image; GIF89a / 87a)
+
+def gif_lzw(indices: bytes, min_size: int, clear_every: int = 0) -> bytes:
+    """LZW data sub-blocks of one raster: a clear code first, the code width growing with the table (12 bits at
+    most, a clear when it is full, or every `clear_every` codes), the end code last."""
+    clear, end = 1 << min_size, (1 << min_size) + 1
+    out, acc, nbits = bytearray(), 0, 0
+    size = min_size + 1
+
+    def emit(code):
+        nonlocal acc, nbits
+        acc |= code << nbits
+        nbits += size
+        while nbits >= 8:
+            out.append(acc & 0xFF)
+            acc >>= 8
+            nbits -= 8
+
+    def reset():
+        return {bytes([i]): i for i in range(clear)}, clear + 2
+
+    table, nxt = reset()
+    emit(clear)
+    w, emitted = b"", 0
+    for b in indices:
+        wc = w + bytes([b])
+        if wc in table:
+            w = wc
+            continue
+        emit(table[w])
+        emitted += 1
+        if nxt < 4096 and not (clear_every and emitted % clear_every == 0):
+            table[wc] = nxt
+            nxt += 1
+            if nxt - 1 == (1 << size) and size < 12:
+                size += 1
+        else:
+            emit(clear)
+            size = min_size + 1
+            table, nxt = reset()
+        w = bytes([b])
+    if w:
+        emit(table[w])
+    emit(end)
+    if nbits:
+        out.append(acc & 0xFF)
+    blocks = bytearray()
+    for i in range(0, len(out), 255):
+        chunk = out[i:i + 255]
+        blocks += bytes([len(chunk)]) + chunk
+    return bytes(blocks) + b"\0"
+
+
+def _gif_table(pal: np.ndarray, bits: int) -> bytes:
+    t = np.zeros((1 << bits, 3), np.uint8)
+    t[:len(pal)] = pal[: 1 << bits]
+    return t.tobytes()
+
+
+def gif_bytes(idx: np.ndarray, pal: np.ndarray, *, local: bool = False, interlace: bool = False, version: bytes = b"89a",
+              transparent: int | None = None, bgindex: int = 0, screen: tuple | None = None, offset=(0, 0),
+              extras: bytes = b"", clear_every: int = 0, bits: int = 8) -> bytes:
+    """idx uint8 [h, w] into `pal` (n x 3); the image at `offset` of a logical screen (default: the image)."""
+    h, w = idx.shape
+    sw, sh = screen or (w + offset[0], h + offset[1])
+    g = b"GIF" + version + struct.pack("<HHBBB", sw, sh, 0 if local else 0x80 | (bits - 1), bgindex, 0)
+    if not local:
+        g += _gif_table(pal, bits)
+    g += extras
+    if transparent is not None:
+        g += b"\x21\xF9\x04\x01\x00\x00" + bytes([transparent]) + b"\0"
+    rows = idx
+    if interlace:
+        order = list(range(0, h, 8)) + list(range(4, h, 8)) + list(range(2, h, 4)) + list(range(1, h, 2))
+        rows = idx[order]
+    flags = (0x40 if interlace else 0) | ((0x80 | (bits - 1)) if local else 0)
+    g += b"\x2C" + struct.pack("<HHHHB", offset[0], offset[1], w, h, flags)
+    if local:
+        g += _gif_table(pal, bits)
+    g += bytes([max(2, bits)]) + gif_lzw(rows.astype(np.uint8).tobytes(), max(2, bits), clear_every)
+    return g + b"\x3B"
+
+
+def gif_variants(arr: np.ndarray, seed: int = 0) -> dict[str, bytes]:
+    rng = np.random.default_rng(seed)
+    h, w, _ = arr.shape
+    out = {}
+    pal = rng.integers(0, 256, size=(256, 3), dtype=np.uint8)
+    idx = rng.integers(0, 256, size=(h, w), dtype=np.uint8)
+    out["g_global.gif"] = gif_bytes(idx, pal)
+    out["g_local_interlaced.gif"] = gif_bytes(idx, pal, local=True, interlace=True)
+    out["g_87a_4bit.gif"] = gif_bytes(idx & 15, pal, version=b"87a", bits=4)
+    out["g_2bit_runs.gif"] = gif_bytes(np.repeat(idx[:, :1] & 3, w, axis=1), pal, bits=2)
+    out["g_transparent_bg.gif"] = gif_bytes(idx & 7, pal, transparent=3, bgindex=5, bits=3,
+                                            screen=(w + 3, h + 2), offset=(2, 1))
+    out["g_local_transparent.gif"] = gif_bytes(idx & 7, pal, local=True, transparent=0, bits=3)
+    out["g_clears.gif"] = gif_bytes(idx, pal, clear_every=37)
+    ext = b"\x21\xFE\x05hello\0" + b"\x21\xFF\x0BNETSCAPE2.0\x03\x01\x00\x00\0"
+    out["g_extensions.gif"] = gif_bytes(idx & 63, pal, extras=ext, bits=6)
+    if Image is not None:
+        out["pil_P.gif"] = pil_bytes(arr, "GIF")
+        out["pil_L_interlace.gif"] = pil_bytes(arr, "GIF", mode="L", interlace=True)
+    return out
+
+
+# ---------------------------------------------------------------- Photoshop PSD
+
+def _packbits(row: bytes) -> bytes:
+    out, i, n = bytearray(), 0, len(row)
+    while i < n:
+        j = i
+        while j + 1 < n and row[j + 1] == row[i] and j - i < 127:
+            j += 1
+        if j > i:                                  # a run of j - i + 1
+            out += bytes([257 - (j - i + 1), row[i]])
+            i = j + 1
+            continue
+        j = i
+        while j < n and j - i < 128 and not (j + 1 < n and row[j + 1] == row[j]):
+            j += 1
+        j = max(j, i + 1)
+        out += bytes([j - i - 1]) + row[i:j]
+        i = j
+    return bytes(out)
+
+
+def psd_bytes(planes: np.ndarray, *, depth: int = 8, rle: bool = False, mode: int = 3, extra: bytes = b"") -> bytes:
+    """planes [c, h, w] (uint8, or uint16 for depth 16), channel by channel."""
+    c, h, w = planes.shape
+    b = b"8BPS" + struct.pack(">H6xHIIHH", 1, c, h, w, depth, mode)
+    b += struct.pack(">I", len(extra)) + extra + struct.pack(">I", 0) + struct.pack(">I", 0)
+    if not rle:
+        dt = ">u2" if depth == 16 else "u1"
+        return b + struct.pack(">H", 0) + planes.astype(dt).tobytes()
+    rows = [_packbits(planes[k, y].astype(np.uint8).tobytes()) for k in range(c) for y in range(h)]
+    return b + struct.pack(">H", 1) + b"".join(struct.pack(">H", len(r)) for r in rows) + b"".join(rows)
+
+
+def psd_variants(arr: np.ndarray, seed: int = 0) -> dict[str, bytes]:
+    rng = np.random.default_rng(seed)
+    h, w, _ = arr.shape
+    rgb = np.moveaxis(arr, 2, 0)
+    alpha = rng.integers(0, 256, size=(1, h, w), dtype=np.uint8)
+    alpha[0, :, ::3] = 255
+    alpha[0, ::4, :] = 0
+    runs = np.repeat(rgb[:, :, :1], w, axis=2)
+    out = {}
+    out["p_rgb.psd"] = psd_bytes(rgb)
+    out["p_rgba.psd"] = psd_bytes(np.concatenate([rgb, alpha]))
+    out["p_rgb_rle.psd"] = psd_bytes(rgb, rle=True)
+    out["p_runs_rle.psd"] = psd_bytes(runs, rle=True)
+    out["p_rgba_rle.psd"] = psd_bytes(np.concatenate([rgb, alpha]), rle=True, extra=b"\0" * 7)
+    out["p_5ch.psd"] = psd_bytes(np.concatenate([rgb, alpha, alpha[:, ::-1]]))
+    out["p_grey1ch.psd"] = psd_bytes(rgb[:1])
+    out["p_2ch_rle.psd"] = psd_bytes(rgb[:2], rle=True)
+    out["p_rgb16.psd"] = psd_bytes(rgb.astype(np.uint16) * 257 + rng.integers(0, 257, size=rgb.shape), depth=16)
+    out["p_rgba16.psd"] = psd_bytes(np.concatenate([rgb, alpha]).astype(np.uint16) * 256 + 128, depth=16)
+    out["p_cmyk.psd"] = psd_bytes(rgb, mode=4)   # not RGB: a failed load
+    return out
+
+
+# ---------------------------------------------------------------- Softimage PIC
+
+def _pic_header(w: int, h: int) -> bytes:
+    return (b"\x53\x80\xF6\x34" + struct.pack(">f", 3.71) + b"made for tests".ljust(80, b"\0") + b"PICT"
+            + struct.pack(">HHfHH", w, h, 1.0, 3, 0))
+
+
+def _pic_values(px: np.ndarray, mask: int) -> bytes:
+    """the channels of `mask` (0x80 R, 0x40 G, 0x20 B, 0x10 A) of pixels px [n, 4], in that order"""
+    cols = [k for k in range(4) if mask & (0x80 >> k)]
+    return px[:, cols].astype(np.uint8).tobytes()
+
+
+def _pic_row(px: np.ndarray, mask: int, kind: int) -> bytes:
+    n = len(px)
+    if kind == 0:
+        return _pic_values(px, mask)
+    out, i = bytearray(), 0
+    while i < n:
+        j = i
+        while j + 1 < n and np.array_equal(px[j + 1], px[i]) and j - i < (254 if kind == 1 else 300):
+            j += 1
+        run = j - i + 1
+        if kind == 1:                                  # pure RLE: count, value
+            out += bytes([run]) + _pic_values(px[i:i + 1], mask)
+        elif run > 1:                                  # mixed RLE: a repeat
+            out += (bytes([run + 127]) if run <= 128 else b"\x80" + struct.pack(">H", run)) + _pic_values(px[i:i + 1], mask)
+        else:                                          # mixed RLE: raw texels up to the next repeat
+            j = i
+            while j + 1 < n and j - i < 127 and not np.array_equal(px[j + 1], px[j]):
+                j += 1
+            run = j - i + 1
+            out += bytes([run - 1]) + _pic_values(px[i:i + run], mask)
+        i += run
+    return bytes(out)
+
+
+def pic_bytes(rgba: np.ndarray, packets: list[tuple[int, int]]) -> bytes:
+    """rgba [h, w, 4]; packets: (channel mask, type 0 raw / 1 pure RLE / 2 mixed RLE), chained in order"""
+    h, w, _ = rgba.shape
+    b = _pic_header(w, h)
+    for k, (mask, kind) in enumerate(packets):
+        b += bytes([1 if k + 1 < len(packets) else 0, 8, kind, mask])
+    for y in range(h):
+        for mask, kind in packets:
+            b += _pic_row(rgba[y], mask, kind)
+    return b
+
+
+def pic_variants(arr: np.ndarray, seed: int = 0) -> dict[str, bytes]:
+    rng = np.random.default_rng(seed)
+    h, w, _ = arr.shape
+    a = rng.integers(0, 256, size=(h, w, 1), dtype=np.uint8)
+    rgba = np.concatenate([arr, a], axis=2)
+    runs = rgba.copy()
+    runs[:, : w // 2] = runs[:, :1]
+    out = {}
+    out["raw.pic"] = pic_bytes(rgba, [(0xE0, 0)])
+    out["raw_alpha.pic"] = pic_bytes(rgba, [(0xE0, 0), (0x10, 0)])
+    out["pure.pic"] = pic_bytes(runs, [(0xE0, 1)])
+    out["mixed.pic"] = pic_bytes(runs, [(0xE0, 2), (0x10, 2)])
+    out["mixed_long.pic"] = pic_bytes(np.repeat(rgba[:, :1], w, axis=1), [(0xF0, 2)])
+    out["split_channels.pic"] = pic_bytes(runs, [(0x80, 1), (0x40, 2), (0x20, 0)])
+    out["green_only.pic"] = pic_bytes(rgba, [(0x40, 0)])
+    return out
+
+
 def corpus(seed: int = 0, h: int = 37, w: int = 53) -> dict[str, bytes]:
     """Every variant, for one picture size."""
     arr = picture(h, w, seed)
@@ -376,4 +606,7 @@ def corpus(seed: int = 0, h: int = 37, w: int = 53) -> dict[str, bytes]:
     files.update(bmp_variants(arr, seed))
     files.update(tga_variants(arr, seed))
     files.update(hdr_variants(seed))
+    files.update(gif_variants(arr, seed))
+    files.update(psd_variants(arr, seed))
+    files.update(pic_variants(arr, seed))
     return files

@@ -9,7 +9,8 @@ Pinning: the reference's own loader is compiled from /root/reference into oracle
 twice with its uninitialised memory made explicit (zeros / a pattern: oracle/stbi_ref.cpp).  Every file of
 tests/image_corpus.py (JPEG baseline / progressive / restart / grey / CMYK, PNG of every colour type and bit
 depth, Adam7, all filters and DEFLATE block types, BMP 1-32 bit with bit fields and V4 / V5 / OS/2 headers,
-TGA raw / RLE / colour-mapped / 16-bit, HDR flat / RLE) and thousands of truncated or corrupted copies must
+TGA raw / RLE / colour-mapped / 16-bit, HDR flat / RLE, GIF global / local / interlaced / transparent / with
+table clears, PSD raw / RLE at 8 and 16 bits with 1-5 channels, Softimage PIC raw / pure / mixed RLE packets) and thousands of truncated or corrupted copies must
 decode to the same bits as the zero build, and as the as-is build wherever the two explicit builds agree.
 Without /root/reference (the GPU box) the committed fixtures under tests/golden/images pin the same path:
 files plus the SHA-256 of the reference loader's output (tools/gen_image_golden.py).
@@ -78,7 +79,8 @@ def same(a, b) -> bool:
 
 def agrees_with_reference(path) -> tuple[bool, bool]:
     """(rt_image_load == the reference loader, the reference's output depends on memory it never wrote).
-    A zero-area image, which stb returns for some corrupt headers, is a failed load here (image_load.cpp)."""
+    A zero-area image, which stb returns for some corrupt headers, is a failed load here (image_load.cpp), and so
+    is a corrupt PIC file on which stb faults (the checker reports the fault as a failed load: oracle/stbi_ref.cpp)."""
     got = load_or_code(path)
     zero, pattern, asis = (stbi_loadf(path, v) for v in ("_zero", "_pattern", ""))
     if zero is not None and zero.size == 0:
@@ -215,16 +217,80 @@ def test_corrupt_and_unknown_files_are_the_reference_failed_load(tmp_path, paylo
 
 @pytest.mark.parametrize("payload", [b"GIF89a\x01\x00\x01\x00\x00\x00\x00;", b"8BPS\x00\x01" + b"\0" * 30,
                                      b"\x53\x80\xF6\x34" + b"\0" * 84 + b"PICT" + b"\0" * 16])
-def test_formats_this_build_does_not_decode_are_unsupported(tmp_path, payload):
-    # GIF, PSD and Softimage PIC: stb would decode them; this build says so loudly instead of guessing
+def test_gif_psd_pic_headers_without_a_picture_are_failed_loads(tmp_path, payload):
+    # a GIF with no colour table and no image, a PSD of version 0, a PIC of zero area: stb fails (or returns a
+    # zero-area image, which this build treats as a failed load) — a magenta texture, the world stays valid
     f = tmp_path / "earthmap.jpg"
     f.write_bytes(payload)
-    with pytest.raises(rt.RenderError) as e:
-        rt.load_image(f)
-    assert e.value.code == -6
+    assert rt.load_image(f) is None
     w = rt.World()
-    w.image(str(f))
-    assert w.status() == -6
+    m = w.image(str(f))
+    assert w.status() == 0 and m.kind == 0
+
+
+def _rgb_float(rgb8: np.ndarray) -> np.ndarray:
+    return ldr_to_float(rgb8)
+
+
+def test_gif_decodes_the_picture_it_encodes(tmp_path):
+    # independent of stb: palette entries of the raster's indices, interlaced or not, global or local table,
+    # with table clears, and the image at an offset of a larger screen (texels outside it: black, or the
+    # background entry's bytes in stored order when its index is not 0)
+    rng = np.random.default_rng(4)
+    idx = rng.integers(0, 256, size=(11, 19), dtype=np.uint8)
+    pal = rng.integers(0, 256, size=(256, 3), dtype=np.uint8)
+    for kw in ({}, {"interlace": True}, {"local": True, "interlace": True}, {"clear_every": 5}):
+        f = tmp_path / "a.gif"
+        f.write_bytes(corpus.gif_bytes(idx, pal, **kw))
+        got = rt.load_image(f)
+        check_vs_stb(f, got)
+        assert np.array_equal(got.view(np.uint32), _rgb_float(pal[idx]).view(np.uint32)), kw
+    f = tmp_path / "b.gif"
+    f.write_bytes(corpus.gif_bytes(idx & 7, pal, bits=3, screen=(22, 13), offset=(2, 1), bgindex=5))
+    got = rt.load_image(f)
+    check_vs_stb(f, got)
+    want = np.empty((13, 22, 3), np.uint8)
+    want[:] = pal[5][::-1]                       # the background entry as stb copies it: blue, green, red
+    want[1:12, 2:21] = pal[idx & 7]
+    assert np.array_equal(got.view(np.uint32), _rgb_float(want).view(np.uint32))
+    f.write_bytes(corpus.gif_bytes(idx & 7, pal, bits=3, transparent=2))
+    got = rt.load_image(f)
+    check_vs_stb(f, got)
+    want = pal[idx & 7].copy()
+    want[(idx & 7) == 2] = 0                     # transparent texels are not written
+    assert np.array_equal(got.view(np.uint32), _rgb_float(want).view(np.uint32))
+
+
+def test_psd_and_pic_decode_the_picture_they_encode(tmp_path):
+    # independent of stb: planar RGB (raw / PackBits, 8 / 16 bits), PIC raw and RLE packets; PSD alpha below 255
+    # removes the white matte in float arithmetic (c / a + 255 (1 - 1 / a), truncated)
+    pic = corpus.picture(9, 14, seed=6, smooth=False)
+    planes = np.moveaxis(pic, 2, 0)
+    cases = {"a.psd": corpus.psd_bytes(planes), "b.psd": corpus.psd_bytes(planes, rle=True),
+             "c.psd": corpus.psd_bytes(planes.astype(np.uint16) * 256 + 255, depth=16),
+             "d.pic": corpus.pic_bytes(np.concatenate([pic, pic[:, :, :1]], 2), [(0xE0, 0)]),
+             "e.pic": corpus.pic_bytes(np.concatenate([pic, pic[:, :, :1]], 2), [(0x80, 1), (0x60, 2)])}
+    for name, data in cases.items():
+        f = tmp_path / name
+        f.write_bytes(data)
+        got = rt.load_image(f)
+        check_vs_stb(f, got)
+        assert np.array_equal(got.view(np.uint32), _rgb_float(pic).view(np.uint32)), name
+    a = np.full((1, 9, 14), 128, np.uint8)
+    f = tmp_path / "f.psd"
+    f.write_bytes(corpus.psd_bytes(np.concatenate([planes, a])))
+    got = rt.load_image(f)
+    check_vs_stb(f, got)
+    ra = np.float32(1) / (np.float32(128) / np.float32(255))
+    v = (pic.astype(np.float32) * ra + np.float32(255) * (np.float32(1) - ra)).astype(np.int32).astype(np.uint8)
+    assert np.array_equal(got.view(np.uint32), _rgb_float(v).view(np.uint32))
+    f = tmp_path / "g.pic"
+    f.write_bytes(corpus.pic_bytes(np.concatenate([pic, pic[:, :, :1]], 2), [(0x40, 0)]))   # green only: others 255
+    want = np.full_like(pic, 255)
+    want[:, :, 1] = pic[:, :, 1]
+    got = rt.load_image(f)
+    check_vs_stb(f, got)
+    assert np.array_equal(got.view(np.uint32), _rgb_float(want).view(np.uint32))
 
 
 def test_earth_scene_loads_its_texture(tmp_path, monkeypatch, picture):

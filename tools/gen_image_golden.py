@@ -19,7 +19,8 @@ from test_image_load import stbi_loadf  # noqa: E402
 PICKS = ["ss2_q75.jpg", "ss0_q100.jpg", "progressive_420.jpg", "restart.jpg", "cmyk.jpg", "grey_progressive.jpg",
          "rgb16_adam7.png", "pal4_flat.png", "grey2_adam7.png", "ga16_flat.png", "rgb8_fixed.png", "rgb8_stored.png",
          "rgb565_bitfields.bmp", "pal4.bmp", "os2_24.bmp", "pal1_topdown.bmp", "v5_32.bmp", "pil_P_tga_rle.tga", "cmap16.tga",
-         "rgb15_topdown_id.tga", "rle.hdr", "flat_wide.hdr"]
+         "rgb15_topdown_id.tga", "rle.hdr", "flat_wide.hdr", "g_local_interlaced.gif", "g_transparent_bg.gif",
+         "g_clears.gif", "p_rgba_rle.psd", "p_rgb16.psd", "mixed.pic", "split_channels.pic"]
 
 
 def main():
