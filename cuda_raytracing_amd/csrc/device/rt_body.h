@@ -1438,6 +1438,30 @@ struct MixedTraceK {
       }
 #endif
       if (!walking) continue;
+#ifdef RT_MIX_KIND
+      // kind-scheduled trips (A/B: RT_JIT_OPTS=-DRT_MIX_KIND=1): the step each walking lane would take next is one of
+      // four classes — a reference BVH node, a transform (a fused / packed chain or an enter / exit), any other
+      // reference record, a step of a macro's SAH walk — and a trip runs one class only, the one most lanes hold (ties:
+      // the lower class), so the wave issues one step body per trip instead of one per class present.  The other
+      // lanes wait a trip; every lane still takes its own steps in its own order, with its own in-place drift.
+      if (!in_macro && T.sp == 0) { walking = false; continue; }
+      {
+        uint32_t cls = 3u;
+        if (!in_macro) {
+          const uint32_t k = S.w4(static_cast<uint32_t>(stk[(T.sp - 1) * 64]) * kNodeWords).x;
+          cls = k == K_BVH ? 0u : ((k == K_TRANSLATE || k == K_YROTATE) ? 1u : 2u);
+        }
+        const uint32_t n0 = static_cast<uint32_t>(__popcll(__ballot(cls == 0u)));
+        const uint32_t n1 = static_cast<uint32_t>(__popcll(__ballot(cls == 1u)));
+        const uint32_t n2 = static_cast<uint32_t>(__popcll(__ballot(cls == 2u)));
+        const uint32_t n3 = static_cast<uint32_t>(__popcll(__ballot(cls == 3u)));
+        uint32_t sel = 0u, best_n = n0;
+        if (n1 > best_n) { sel = 1u; best_n = n1; }
+        if (n2 > best_n) { sel = 2u; best_n = n2; }
+        if (n3 > best_n) sel = 3u;
+        if (cls != sel) continue;
+      }
+#endif
       if (!in_macro) {
         if (T.sp == 0) { walking = false; continue; }
         // ---- one step of the reference walk (trav_step), macro roots aside ----
