@@ -1030,12 +1030,20 @@ struct AccelTraceK {
           // sphere inline evicted the frame's lines from L2 before their tiles had filled them: twice the memory
           // writes)
           const uint2 *L = reinterpret_cast<const uint2 *>(A.prim_lists) + static_cast<size_t>(tile) * cap;
-          uint2 c1 = n > 0 ? L[0] : make_uint2(0, 0);
+#ifdef RT_NT_LISTS   // A/B (RT_JIT_OPTS=-DRT_NT_LISTS): list entries read with the non-temporal hint (L2 streaming)
+          auto entry = [&](uint32_t k) -> uint2 {
+            const unsigned long long v = __builtin_nontemporal_load(reinterpret_cast<const unsigned long long *>(L + k));
+            return make_uint2(static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32));
+          };
+#else
+          auto entry = [&](uint32_t k) -> uint2 { return L[k]; };
+#endif
+          uint2 c1 = n > 0 ? entry(0) : make_uint2(0, 0);
           for (uint32_t k = 0; k < n; ++k) {
             const uint2 c = c1;
             if (__uint_as_float(c.y) > __builtin_fmaf(T.tmax, dl, rho) * 1.0000010f) break;
             const uint4 a0 = P[c.x * 4], a1 = P[c.x * 4 + 1];
-            if (k + 1 < n) c1 = L[k + 1];
+            if (k + 1 < n) c1 = entry(k + 1);
             if (COUNT) vc.xp++;
             if (sphere_hit_tie<UV, true, false>(T, r, h, 0u, mk(asf(a0.x), asf(a0.y), asf(a0.z)),
                                                 mk(asf(a0.w), asf(a1.x), asf(a1.y)), asf(a1.z), 0.0f, sa2, sra2, tie))
