@@ -2130,12 +2130,28 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const uint32_t try_cap = A.max_tries ? A.max_tries : 0xffffffffu;
   // the pixel's viewport point (:1565-1567), recomputed per sample from pxy (a few ops and no division; three
   // fewer registers carried across the trace)
+#ifndef RT_KARGS_HOLD
+  // The kernel arguments of the camera and of the tile / pixel pickup are re-read from the kernarg segment (scalar
+  // loads) where they are used — once per sample and once per tile — instead of held in SGPRs across the render loop:
+  // every kernel takes RenderArgs as its only argument, at offset 0, and the asm hides the pointer's provenance, so no
+  // earlier load is kept live.  SGPRs spilled into VGPR lanes (v_writelane / v_readlane, VALU instructions): scene 0
+  // 27 -> 7, Perlin 120 -> 52 (RT_JIT_OPTS=-DRT_KARGS_HOLD restores the held form for A/Bs)
+  auto cam = [&]() {
+    typedef const __attribute__((address_space(4))) RenderArgs *KPtr;
+    KPtr K = (KPtr)(__builtin_amdgcn_kernarg_segment_ptr());
+    asm volatile("" : "+s"(K));
+    return K;
+  };
+#else
+  auto cam = [&]() { return &A; };
+#endif
   auto pixel_point = [&]() -> f3 {
     const int32_t lr = static_cast<int32_t>(pxy >> 16), j = static_cast<int32_t>(pxy & 0xffffu);
     const int32_t i = A.row_offset + lr * A.row_stride;
-    return add(mk(A.p00[0], A.p00[1], A.p00[2]),
-             add(scale(static_cast<float>(i), mk(A.dv[0], A.dv[1], A.dv[2])),
-                 scale(static_cast<float>(j), mk(A.du[0], A.du[1], A.du[2]))));
+    const auto C = cam();
+    return add(mk(C->p00[0], C->p00[1], C->p00[2]),
+             add(scale(static_cast<float>(i), mk(C->dv[0], C->dv[1], C->dv[2])),
+                 scale(static_cast<float>(j), mk(C->du[0], C->du[1], C->du[2]))));
   };
   // the scene-specialised kernels (register room at 72-85 VGPRs) keep the point from the pixel's pickup instead of
   // recomputing it for every sample; the walks at a register budget (the verified sphere walk's 80, the mixed
@@ -2143,8 +2159,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   constexpr bool kCarryPoint = carry_point<Trace>(0);
   f3 pp = mk(0, 0, 0);
   auto camera_ray = [&]() {                                                 // :1561-1578
-    if (A.defocus_angle <= 0) {
-      ray.o = mk(A.center[0], A.center[1], A.center[2]);
+    const auto C = cam();
+    if (C->defocus_angle <= 0) {
+      ray.o = mk(C->center[0], C->center[1], C->center[2]);
     } else {                                                                // :1459-1476
       float x, y;
       for (;;) {
@@ -2153,15 +2170,16 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         float l = sqrtf(x * x + y * y + 0.0f * 0.0f);
         if (l * l < 1.0f) break;
       }
-      f3 c = mk(A.center[0], A.center[1], A.center[2]);
-      f3 u = mk(A.dfu[0], A.dfu[1], A.dfu[2]), v = mk(A.dfv[0], A.dfv[1], A.dfv[2]);
+      f3 c = mk(C->center[0], C->center[1], C->center[2]);
+      f3 u = mk(C->dfu[0], C->dfu[1], C->dfu[2]), v = mk(C->dfv[0], C->dfv[1], C->dfv[2]);
       ray.o = add(c, add(scale(x, u), scale(y, v)));
     }
     float xo = rng.uniform() - 0.5f;
     float yo = rng.uniform() - 0.5f;
     ray.d = sub(kCarryPoint ? pp : pixel_point(), ray.o);
-    ray.d = add(ray.d, scale(xo, mk(A.du[0], A.du[1], A.du[2])));
-    ray.d = add(ray.d, scale(yo, mk(A.dv[0], A.dv[1], A.dv[2])));
+    const auto D = cam();
+    ray.d = add(ray.d, scale(xo, mk(D->du[0], D->du[1], D->du[2])));
+    ray.d = add(ray.d, scale(yo, mk(D->dv[0], D->dv[1], D->dv[2])));
     ray.time = rng.uniform();
     depth = 0;
     rsp = 0;
@@ -2198,51 +2216,52 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
     const bool sparse = A.prio_lanes < static_cast<uint32_t>(kChunk);
     uint32_t nhot = sparse ? static_cast<uint32_t>(__popcll(__ballot(busy && hot))) : 0u;
     while (m != 0 && !exhausted) {
+      const auto K = cam();   // tile / pixel pickup: kernel arguments read here (see cam)
       if (chunk_pos >= chunk_end) {
         if (n_stage != 0u) stage_store();   // the wave's finished tiles first (their slots become free)
-        if (sparse && !A.prio_mix && (nhot >= A.prio_lanes || (nhot > 0 && prio_done))) break;
+        if (sparse && !K->prio_mix && (nhot >= K->prio_lanes || (nhot > 0 && prio_done))) break;
         // the costliest tiles (the first prio_ids ids of the longest-first order) may be handed out in
         // prio_chunk-pixel pieces from their own counter, so that their long pixel chains spread over
-        // more waves; every other tile goes out whole.  Mixed (A.prio_mix): a wave holding prio_lanes of
+        // more waves; every other tile goes out whole.  Mixed (K->prio_mix): a wave holding prio_lanes of
         // those pixels takes ordinary tiles for its other lanes meanwhile.
         uint32_t base = 0, size = static_cast<uint32_t>(kChunk), hold = 0;
-        const bool capped = A.prio_mix && nhot >= A.prio_lanes;
-        const bool split = A.prio_chunk < static_cast<uint32_t>(kChunk) && !prio_done && !capped;
+        const bool capped = K->prio_mix && nhot >= K->prio_lanes;
+        const bool split = K->prio_chunk < static_cast<uint32_t>(kChunk) && !prio_done && !capped;
         if (lane == 0) {
-          if (split) base = atomicAdd(A.work + 1, A.prio_chunk);
-          if (!split || base >= A.prio_ids) {
-            if (sparse && !A.prio_mix && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
-            else if (!A.cls_off) {
-              base = atomicAdd(A.work, static_cast<uint32_t>(kChunk)) + (A.prio_chunk < static_cast<uint32_t>(kChunk) ? A.prio_ids : 0u);
+          if (split) base = atomicAdd(K->work + 1, K->prio_chunk);
+          if (!split || base >= K->prio_ids) {
+            if (sparse && !K->prio_mix && nhot > 0) hold = 1;   // the last costly pixels are out: stay sparse
+            else if (!K->cls_off) {
+              base = atomicAdd(K->work, static_cast<uint32_t>(kChunk)) + (K->prio_chunk < static_cast<uint32_t>(kChunk) ? K->prio_ids : 0u);
               // the last tail_ids ids of the order go out in tail_chunk-pixel pieces from their own counter: a wave
               // then holds at most tail_chunk - 1 pixels it has not started when the queue drains, instead of up to 63
               // of a whole tile, so the waves' last pixels start (and the waves end) closer together
-              if ((F & kVarTail) != 0 && A.tail_ids != 0u && base >= A.n_ids - A.tail_ids) {
-                base = A.n_ids - A.tail_ids + atomicAdd(A.work + kTailWord, A.tail_chunk);
-                size = A.tail_chunk;
+              if ((F & kVarTail) != 0 && K->tail_ids != 0u && base >= K->n_ids - K->tail_ids) {
+                base = K->n_ids - K->tail_ids + atomicAdd(K->work + kTailWord, K->tail_chunk);
+                size = K->tail_chunk;
               }
             }
           } else {
-            size = A.prio_chunk;
+            size = K->prio_chunk;
           }
         }
-        if (A.cls_off) {
+        if (K->cls_off) {
           // XCD classes (whole tiles only): this wave's XCD queue — tiles whose frame lines no other XCD writes, so the
           // XCD's L2 merges their partial lines into whole ones — then, once it is drained, the other queues in turn.
           // Wave-uniform (scalar registers); lane 0 takes the ids
           for (;;) {
             const uint32_t q = (xcd + cls_step) & (kXcdClasses - 1u);
-            const uint32_t lo = A.cls_off[q], hi = A.cls_off[q + 1];   // positions in the tile order
+            const uint32_t lo = K->cls_off[q], hi = K->cls_off[q + 1];   // positions in the tile order
             uint32_t b = 0;
-            if (lane == 0) b = atomicAdd(A.work + kClsWord + q, static_cast<uint32_t>(kChunk));
+            if (lane == 0) b = atomicAdd(K->work + kClsWord + q, static_cast<uint32_t>(kChunk));
             b = __builtin_amdgcn_readfirstlane(b);
             if (b < (hi - lo) * static_cast<uint32_t>(kChunk)) {
               base = lo * static_cast<uint32_t>(kChunk) + b;
               // the chunk is among the costliest if its rank in its class is (each class holds ~1/8 of them)
-              chunk_hot = b < A.prio_ids / kXcdClasses;
+              chunk_hot = b < K->prio_ids / kXcdClasses;
               break;
             }
-            if (++cls_step == kXcdClasses) { base = A.n_ids; break; }
+            if (++cls_step == kXcdClasses) { base = K->n_ids; break; }
           }
         }
         base = __builtin_amdgcn_readfirstlane(__shfl(base, 0));
@@ -2252,11 +2271,11 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         if (hold) break;
         // a capped mixed wave that finds the ordinary tiles gone waits for a hot lane to free (costly
         // pixels may still be queued); the queue is exhausted only when both counters are drained
-        if (base >= A.n_ids) { if (!capped) exhausted = true; break; }
-        if (A.reverse_tiles) base = A.n_ids - kChunk - base;   // whole tiles: n_ids is a multiple of 64
+        if (base >= K->n_ids) { if (!capped) exhausted = true; break; }
+        if (K->reverse_tiles) base = K->n_ids - kChunk - base;   // whole tiles: n_ids is a multiple of 64
         tiles_taken++;
         chunk_pos = base;
-        chunk_end = min(base + size, A.n_ids);
+        chunk_end = min(base + size, K->n_ids);
         if (!probe) {
           // RNG seeding of the chunk (init_gpu_data's curand_init, :1591-1606, subsequence = global pixel index
           // i * W + j): lane l takes id base + l, starts from the phase base of its pixel (the row's state jumped
@@ -2269,12 +2288,12 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
           bool valid = false;
           if (id < chunk_end) {
             const uint32_t kk = id & 63u;
-            if (A.tile_order) tile = A.tile_order[tile];
-            const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
+            if (K->tile_order) tile = K->tile_order[tile];
+            const uint32_t ty = tile / K->tiles_x, tx = tile - ty * K->tiles_x;
             const uint32_t lr = (ty << tsh) + (kk >> ts), j = (tx << ts) + (kk & twm);
-            if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
+            if (lr < K->rows && j < static_cast<uint32_t>(K->width)) {
               // phase base of (lr, j & (tw - 1)) and the column table of J^(tw (j >> ts)): one table per tile
-              const uint32_t *pb = A.rng_rows + ((lr << ts) + (j & twm)) * 8;
+              const uint32_t *pb = K->rng_rows + ((lr << ts) + (j & twm)) * 8;
               const uint4 rb = *reinterpret_cast<const uint4 *>(pb);
               x0 = rb.x; x1 = rb.y; x2 = rb.z; x3 = rb.w; x4 = pb[4];
               tcol = j >> ts;
@@ -2294,7 +2313,7 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
               stage_next = stage_next + 1u == n_stage ? 0u : stage_next + 1u;
             }
           }
-          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(A.rng_nib), 0,
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(K->rng_nib), 0,
                                                                               0x7fffffff, 0x00020000);
           // two table products (J^(tw (t & 15)), then J^(16 tw (t >> 4))): 16 + W / (16 tw) tables in all, so each
           // XCD's L2 fetches a few hundred KB of them instead of every column group's table
@@ -2318,34 +2337,34 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
         const uint32_t id = chunk_pos + rank;
         uint32_t tile, k, salt = 0;
         if (probe) {                        // probe: probe_per_tile paths spread over the tile's pixels
-          tile = id / A.probe_per_tile;
-          const uint32_t q = id - tile * A.probe_per_tile;
+          tile = id / K->probe_per_tile;
+          const uint32_t q = id - tile * K->probe_per_tile;
           k = (q * 37u + 11u) & 63u;        // a permutation of the 64 pixels per 64 paths
           salt = q >> 6;                    // more than 64 paths per tile: another stream per pixel
         } else {
           tile = id >> 6;
           k = id & 63u;
-          if (A.tile_order) tile = A.tile_order[tile];
+          if (K->tile_order) tile = K->tile_order[tile];
         }
-        const uint32_t ty = tile / A.tiles_x, tx = tile - ty * A.tiles_x;
+        const uint32_t ty = tile / K->tiles_x, tx = tile - ty * K->tiles_x;
         const uint32_t lr = (ty << tsh) + (k >> ts), j = (tx << ts) + (k & twm);
-        if (lr < A.rows && j < static_cast<uint32_t>(A.width)) {
+        if (lr < K->rows && j < static_cast<uint32_t>(K->width)) {
           pxy = (lr << 16) | j;
           if constexpr (kCarryPoint) pp = pixel_point();
           need = false;
           busy = true;
-          hot = A.cls_off ? chunk_hot : id < A.prio_ids;
+          hot = K->cls_off ? chunk_hot : id < K->prio_ids;
           if (probe) {                      // throwaway stream: the real ones are not consumed
             probe_tile = tile;
             probe_rounds = 0;
-            uint32_t hsh = (lr * static_cast<uint32_t>(A.width) + j) * 0x9E3779B9u + 0x7F4A7C15u + salt * 0x632BE5ABu;
+            uint32_t hsh = (lr * static_cast<uint32_t>(K->width) + j) * 0x9E3779B9u + 0x7F4A7C15u + salt * 0x632BE5ABu;
             hsh ^= hsh >> 16; hsh *= 0x85EBCA6Bu; hsh ^= hsh >> 13; hsh *= 0xC2B2AE35u; hsh ^= hsh >> 16;
             rng.d = hsh; rng.x0 = hsh ^ 0x2c7f967fu; rng.x1 = hsh * 3u + 1u; rng.x2 = ~hsh;
             rng.x3 = hsh ^ 0xa03697cbu; rng.x4 = hsh | 1u;
           } else {
             // the state seeded at the chunk's pickup (the slot entry of this id)
             const uint32_t so = id & 63u;
-            rng.d = A.rng_d;
+            rng.d = K->rng_d;
             rng.x0 = rng_slot[so];
             rng.x1 = rng_slot[64u + so];
             rng.x2 = rng_slot[128u + so];
