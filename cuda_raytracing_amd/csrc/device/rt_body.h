@@ -503,6 +503,21 @@ __device__ __forceinline__ bool hit_front(const Hit &h) { return h.fd < 0.0f; }
 __device__ __forceinline__ f3 hit_normal(const Hit &h) { return hit_front(h) ? h.n : flip(h.n); }
 struct Visits { uint32_t k[7]; uint32_t max_sp; uint32_t xn, xp; };   // xn / xp: executed SAH node visits / leaf tests
 
+// Kernel arguments read where they are used: every render kernel takes RenderArgs as its only argument (kernarg
+// offset 0), and a pointer to it whose provenance an empty asm hides makes each use a scalar load instead of a value
+// the compiler holds in SGPRs across the render loop (held, the excess spilled into VGPR lanes: DESIGN §5f).
+// RT_JIT_OPTS=-DRT_KARGS_HOLD restores the held form (A/B).
+#ifndef RT_KARGS_HOLD
+typedef const __attribute__((address_space(4))) RenderArgs *KArgsPtr;
+__device__ __forceinline__ KArgsPtr kargs(const RenderArgs &) {
+  KArgsPtr K = (KArgsPtr)(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(K));
+  return K;
+}
+#else
+__device__ __forceinline__ const RenderArgs *kargs(const RenderArgs &A) { return &A; }
+#endif
+
 // locals of hit() (:1082-1088) plus a cached 1/dir
 struct Trav {
   f3 inv;          // 1/dir, refreshed whenever the ray direction changes (y-rotation enter/exit)
@@ -2130,21 +2145,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   const uint32_t try_cap = A.max_tries ? A.max_tries : 0xffffffffu;
   // the pixel's viewport point (:1565-1567), recomputed per sample from pxy (a few ops and no division; three
   // fewer registers carried across the trace)
-#ifndef RT_KARGS_HOLD
-  // The kernel arguments of the camera and of the tile / pixel pickup are re-read from the kernarg segment (scalar
-  // loads) where they are used — once per sample and once per tile — instead of held in SGPRs across the render loop:
-  // every kernel takes RenderArgs as its only argument, at offset 0, and the asm hides the pointer's provenance, so no
-  // earlier load is kept live.  SGPRs spilled into VGPR lanes (v_writelane / v_readlane, VALU instructions): scene 0
-  // 27 -> 7, Perlin 120 -> 52 (RT_JIT_OPTS=-DRT_KARGS_HOLD restores the held form for A/Bs)
-  auto cam = [&]() {
-    typedef const __attribute__((address_space(4))) RenderArgs *KPtr;
-    KPtr K = (KPtr)(__builtin_amdgcn_kernarg_segment_ptr());
-    asm volatile("" : "+s"(K));
-    return K;
-  };
-#else
-  auto cam = [&]() { return &A; };
-#endif
+  // the camera's arguments (once per sample) and the tile / pixel pickup's (once per tile) are read where used (kargs):
+  // held, they pushed the render loop's own SGPRs into VGPR lanes — scene 0 27 -> 7 spilled SGPRs, Perlin 120 -> 52
+  auto cam = [&]() { return kargs(A); };
   auto pixel_point = [&]() -> f3 {
     const int32_t lr = static_cast<int32_t>(pxy >> 16), j = static_cast<int32_t>(pxy & 0xffffu);
     const int32_t i = A.row_offset + lr * A.row_stride;
