@@ -1350,9 +1350,11 @@ constexpr float kMixBoundRel = 1.52587890625e-05f;   // 2^-16
 
 __device__ __forceinline__ bool mix_box(const Trav &T, const SlabRay &R, float x0, float x1, float y0, float y1, float z0,
                                         float z1, float bound, float *tnear) {
-  const float nx = __builtin_fmaf(R.nx ? x1 : x0, T.inv.x, R.on.x), fx = __builtin_fmaf(R.nx ? x0 : x1, T.inv.x, R.of.x);
-  const float ny = __builtin_fmaf(R.ny ? y1 : y0, T.inv.y, R.on.y), fy = __builtin_fmaf(R.ny ? y0 : y1, T.inv.y, R.of.y);
-  const float nz = __builtin_fmaf(R.nz ? z1 : z0, T.inv.z, R.on.z), fz = __builtin_fmaf(R.nz ? z0 : z1, T.inv.z, R.of.z);
+  // the octant from 1/d's signs (SlabRay's flags, recomputed: three registers fewer across the mixed walk)
+  const bool sx = T.inv.x < 0.0f, sy = T.inv.y < 0.0f, sz = T.inv.z < 0.0f;
+  const float nx = __builtin_fmaf(sx ? x1 : x0, T.inv.x, R.on.x), fx = __builtin_fmaf(sx ? x0 : x1, T.inv.x, R.of.x);
+  const float ny = __builtin_fmaf(sy ? y1 : y0, T.inv.y, R.on.y), fy = __builtin_fmaf(sy ? y0 : y1, T.inv.y, R.of.y);
+  const float nz = __builtin_fmaf(sz ? z1 : z0, T.inv.z, R.on.z), fz = __builtin_fmaf(sz ? z0 : z1, T.inv.z, R.of.z);
   const float t0 = fmaxf(fmaxf(nx, ny), fmaxf(nz, kTmin)), t1 = fminf(fminf(fx, fy), fminf(fz, bound));
   *tnear = t0;
   return !(t1 < t0);
@@ -1422,10 +1424,8 @@ struct MixedTraceK {
     bool walking = true, in_macro = false;
     uint32_t mroot = 0, mnode = 0, bprim = 0, bgroup = 0;
     int msp = 0;
-    float tin = 0.0f, best = __builtin_huge_valf(), second = __builtin_huge_valf();
+    float best = __builtin_huge_valf(), second = __builtin_huge_valf();
     bool tie = false;
-    SlabRay sr;
-    sr.on = mk(0, 0, 0); sr.of = mk(0, 0, 0); sr.nx = sr.ny = sr.nz = false;
 #ifdef RT_MIX_DIAG
     // diagnostic build (RT_JIT_OPTS=-DRT_MIX_DIAG): wave trips, lanes per phase, reference steps by kind;
     // every value is wave-uniform (ballots at the top of a trip, where all the wave's walkers are active)
@@ -1597,15 +1597,10 @@ struct MixedTraceK {
               mroot = idx;
               mnode = mw & kMacroRootMask;
               msp = 0;
-              tin = T.tmax;
               best = __builtin_huge_valf();
               second = __builtin_huge_valf();
               bprim = 0; bgroup = kMixNoGroup;
               tie = false;
-              const float pad_o = kAccelKappa * ao;
-              const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
-              const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
-              sr = slab_ray(T, oinv, pinv);
             }
           }
           if (!macro) {
@@ -1625,8 +1620,18 @@ struct MixedTraceK {
         continue;
       }
       // ---- one step of the macro's SAH walk ----
-      const float cur = fminf(best, tin);
-      const float bound = best < __builtin_huge_valf() ? fminf(tin, best + best * kMixBoundRel) : tin;
+      // the padded slab offsets, recomputed every step from the ray (unchanged inside a macro) instead of held: the
+      // same operations on the same values as at the macro's entry, six registers fewer across the walk
+      SlabRay sr;
+      {
+        const float ao = fabsf(r.o.x) + fabsf(r.o.y) + fabsf(r.o.z);
+        const float pad_o = kAccelKappa * ao;
+        const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
+        const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
+        sr = slab_ray(T, oinv, pinv);
+      }
+      const float cur = fminf(best, T.tmax);
+      const float bound = best < __builtin_huge_valf() ? fminf(T.tmax, best + best * kMixBoundRel) : T.tmax;
       const uint4 q0 = N[mnode * 4], q1 = N[mnode * 4 + 1], q2 = N[mnode * 4 + 2], q3 = N[mnode * 4 + 3];
       float n0, n1;
       bool h0 = mix_box(T, sr, asf(q0.x), asf(q0.y), asf(q0.z), asf(q0.w), asf(q1.x), asf(q1.y), bound, &n0);
@@ -1648,12 +1653,12 @@ struct MixedTraceK {
           v = sphere_value(r, mk(asf(p0.z), asf(p0.w), asf(p1.x)), mk(asf(p1.y), asf(p1.z), asf(p1.w)), asf(p2.y), ok);
         } else {
           const uint4 p3 = pw[3], p4 = pw[4];
-          // a candidate matters only at or below the running value (best / tie) or below min(second, tin)
+          // a candidate matters only at or below the running value (best / tie) or below min(second, T.tmax)
           // (the reach proof reads second only through that minimum): others skip the inside test
           v = planar_value(r, p0.x == K_TRIANGLE, mk(asf(p0.z), asf(p0.w), asf(p1.x)), asf(p1.y),
                            mk(asf(p1.z), asf(p1.w), asf(p2.x)), mk(asf(p2.y), asf(p2.z), asf(p2.w)),
                            mk(asf(p3.x), asf(p3.y), asf(p3.z)), mk(asf(p3.w), asf(p4.x), asf(p4.y)), ok,
-                           fmaxf(cur_k, fminf(second, tin)));
+                           fmaxf(cur_k, fminf(second, T.tmax)));
         }
         if (ok) {
           const uint32_t g = pw[5].x;   // MP_GROUP
@@ -1685,10 +1690,10 @@ struct MixedTraceK {
       bool ok = !tie && !A.mix_no_proof;
       const uint4 *bw = P + static_cast<size_t>(bprim) * (kMixPrimWords / 4);
       if (ok && best < __builtin_huge_valf() && bgroup != kMixNoGroup) {
-        const float bnd = fminf(tin, best + best * kMixBoundRel);
+        const float bnd = fminf(T.tmax, best + best * kMixBoundRel);
         const uint4 g0 = bw[5], g1 = bw[6];
         Trav tt = T;
-        tt.tmax = fminf(fminf(tin, second), bnd);
+        tt.tmax = fminf(fminf(T.tmax, second), bnd);
         ok = box_hit(tt, r, asf(g0.y), asf(g0.z), asf(g0.w), asf(g1.x), asf(g1.y), asf(g1.z));
       }
       if (ok) {
