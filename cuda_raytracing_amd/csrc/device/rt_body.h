@@ -1426,6 +1426,8 @@ struct MixedTraceK {
     int msp = 0;
     float best = __builtin_huge_valf(), second = __builtin_huge_valf();
     bool tie = false;
+    SlabRay sr;
+    sr.on = mk(0, 0, 0); sr.of = mk(0, 0, 0); sr.nx = sr.ny = sr.nz = false;
 #ifdef RT_MIX_DIAG
     // diagnostic build (RT_JIT_OPTS=-DRT_MIX_DIAG): wave trips, lanes per phase, reference steps by kind;
     // every value is wave-uniform (ballots at the top of a trip, where all the wave's walkers are active)
@@ -1601,6 +1603,12 @@ struct MixedTraceK {
               second = __builtin_huge_valf();
               bprim = 0; bgroup = kMixNoGroup;
               tie = false;
+#ifndef RT_MIX_SLAB_RECOMPUTE
+              const float pad_o = kAccelKappa * ao;
+              const f3 oinv = mk(r.o.x * T.inv.x, r.o.y * T.inv.y, r.o.z * T.inv.z);
+              const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
+              sr = slab_ray(T, oinv, pinv);
+#endif
             }
           }
           if (!macro) {
@@ -1620,9 +1628,10 @@ struct MixedTraceK {
         continue;
       }
       // ---- one step of the macro's SAH walk ----
-      // the padded slab offsets, recomputed every step from the ray (unchanged inside a macro) instead of held: the
-      // same operations on the same values as at the macro's entry, six registers fewer across the walk
-      SlabRay sr;
+#ifdef RT_MIX_SLAB_RECOMPUTE
+      // A/B (RT_JIT_OPTS=-DRT_MIX_SLAB_RECOMPUTE): the padded slab offsets recomputed every step from the ray (unchanged
+      // inside a macro: the same operations on the same values as at the entry) instead of held — six registers fewer,
+      // so that RT_JIT_WAVES=4 builds the walk at 128 VGPRs without spilling
       {
         const float ao = fabsf(r.o.x) + fabsf(r.o.y) + fabsf(r.o.z);
         const float pad_o = kAccelKappa * ao;
@@ -1630,6 +1639,7 @@ struct MixedTraceK {
         const f3 pinv = mk(pad_o * fabsf(T.inv.x), pad_o * fabsf(T.inv.y), pad_o * fabsf(T.inv.z));
         sr = slab_ray(T, oinv, pinv);
       }
+#endif
       const float cur = fminf(best, T.tmax);
       const float bound = best < __builtin_huge_valf() ? fminf(T.tmax, best + best * kMixBoundRel) : T.tmax;
       const uint4 q0 = N[mnode * 4], q1 = N[mnode * 4 + 1], q2 = N[mnode * 4 + 2], q3 = N[mnode * 4 + 3];

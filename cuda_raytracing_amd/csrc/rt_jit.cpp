@@ -539,7 +539,6 @@ std::string jit_mixed_source(const SceneImage &img, int variant, int waves) {
 // and the Cornell box land at 81-87 VGPRs, the mixed walk of final_scene at 169).
 // RT_JIT_WAVES (explicit) or RT_JIT_RAISE=0 leaves the first build.
 constexpr int kRaiseSlack = 12;
-constexpr int kMixedRaiseSlack = 16;
 // Scratch a raised build may keep: none by default (round 5).  A build forced under its allocator's register count
 // spills VGPRs, and two such builds of the verified sphere walk rendered wrong pixels (and one faulted) where the same
 // source at a budget without VGPR spills was exact — each time a small unrelated source edit flipped it.
@@ -559,8 +558,7 @@ int render_vgprs(hipFunction_t fn, int *scratch) {
 
 // source(n): the module's source with the render kernel's attribute waves_attr_n(n) (n < 0: a cap of -n VGPRs)
 template <class Source>
-void raise_residency(const Source &source, const char *prefix, JitKernels *out, const std::vector<std::string> &extra = {},
-                     int slack = kRaiseSlack, bool by_waves = false) {
+void raise_residency(const Source &source, const char *prefix, JitKernels *out, const std::vector<std::string> &extra = {}) {
   if (std::getenv("RT_JIT_WAVES") || std::getenv("RT_JIT_MAX_VGPR")) return;
   if (const char *e = std::getenv("RT_JIT_RAISE")) if (e[0] == '0') return;
   int sc0 = 0;
@@ -569,12 +567,10 @@ void raise_residency(const Source &source, const char *prefix, JitKernels *out, 
   const int cur = resident_blocks_by_vgprs(v0);
   if (cur >= 8) return;
   const int limit = 512 / (cur + 1) / 16 * 16;   // the hardware's budget for one more wave per SIMD
-  if (v0 - limit > slack) return;
+  if (v0 - limit > kRaiseSlack) return;
   JitKernels k = *out;
   std::string why;
-  // by_waves: ask for the next residency by waves per EU instead of a VGPR cap (the allocator then budgets differently:
-  // the mixed walk fits 128 VGPRs without spilling that way, and spills 36 B under the cap)
-  if (!build_module(source(by_waves ? cur + 1 : -limit), prefix, &k, &why, extra)) return;
+  if (!build_module(source(-limit), prefix, &k, &why, extra)) return;
   int sc = 0;
   const int v = render_vgprs(k.render, &sc);
   if (std::getenv("RT_DEBUG"))
@@ -629,10 +625,7 @@ bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std:
   out->visits = 0;
   out->folded = false;
   if (!build_module(jit_mixed_source(img, variant), "rt_mixed", out, why)) return false;
-  // the mixed walk lands at 144 VGPRs (3 waves / SIMD) and fits 128 (4 waves) without spilling since round 6 (its slab
-  // offsets recomputed per macro step, tin = T.tmax) when asked for 4 waves per EU: a raise from up to 16 VGPRs above
-  // the boundary, by waves
-  raise_residency([&](int w) { return jit_mixed_source(img, variant, w); }, "rt_mixed", out, {}, kMixedRaiseSlack, true);
+  raise_residency([&](int w) { return jit_mixed_source(img, variant, w); }, "rt_mixed", out);
   return true;
 }
 
