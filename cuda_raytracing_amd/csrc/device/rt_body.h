@@ -1933,6 +1933,9 @@ __device__ __forceinline__ void render_body(const RenderArgs &A) {
   if (A.span && blockIdx.x < 8u && threadIdx.x == 0)
     atomicMax(A.span, static_cast<unsigned long long>(~__builtin_amdgcn_s_memrealtime()));
   Mem<LDS> S{A.scene};
+  // kargs() reads RenderArgs from the kernarg segment's start: every kernel must take it as its only argument
+  [[maybe_unused]] const bool kargs_ok = RT_CHECK(A, kargs(A)->scene == A.scene && kargs(A)->n_ids == A.n_ids &&
+                                                        kargs(A)->spp == A.spp, CHK_KARGS, 0u, 1u);
   if (LDS) {
     const uint32_t n4 = A.scene_words / 4;
     const uint4 *src = reinterpret_cast<const uint4 *>(A.scene);

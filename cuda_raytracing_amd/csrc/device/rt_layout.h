@@ -317,7 +317,8 @@ enum CheckSite : uint32_t {
   CHK_RC_DEEP = 5,         // colour-stack level past the LDS ones vs max_bounces
   CHK_POOL_CHUNK = 6,      // a lane's deep-level pool chunk vs rc_pool_chunks
   CHK_PIXEL = 7,           // output pixel / tile index vs the frame
-  CHK__COUNT = 8
+  CHK_KARGS = 8,           // the kernarg segment's RenderArgs (kargs(), rt_body.h) differs from the kernel's argument
+  CHK__COUNT = 9
 };
 
 constexpr uint32_t kProbePerTile = 8;   // default probe paths per 8x8 tile

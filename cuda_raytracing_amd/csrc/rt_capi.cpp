@@ -1361,7 +1361,8 @@ int rt_context_timing(rt_context *c, rt_stats *st) {
     if (ck[0] != rt::CHK_NONE) {
       static const char *const names[rt::CHK__COUNT] = {"none", "lane DFS stack", "verified sphere walk stack",
                                                         "verified mixed walk stack", "colour-stack LDS level",
-                                                        "colour-stack deep level", "deep-level pool chunk", "output pixel"};
+                                                        "colour-stack deep level", "deep-level pool chunk", "output pixel",
+                                                        "kernel-argument re-read"};
       char b[200];
       std::snprintf(b, sizeof b, "device check failed: %s index %u >= capacity %u (site %u)",
                     ck[0] < rt::CHK__COUNT ? names[ck[0]] : "unknown", ck[1], ck[2], ck[0]);
