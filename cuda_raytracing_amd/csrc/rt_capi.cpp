@@ -1552,7 +1552,8 @@ int rt_kernel_build(const rt_scene *scene, int traversal, int32_t max_bounces, r
   const char *prefix = traversal == RT_TRAV_STATIC ? "rt_static" : traversal == RT_TRAV_ACCEL ? "rt_accel"
                      : traversal == RT_TRAV_MIXED ? "rt_mixed" : "rt_lane";
   const std::vector<std::string> extra = traversal == RT_TRAV_STATIC ? rt::static_sched(img)
-                                       : traversal == RT_TRAV_ACCEL ? rt::accel_sched() : std::vector<std::string>{};
+                                       : traversal == RT_TRAV_ACCEL ? rt::accel_sched()
+                                       : traversal == RT_TRAV_MIXED ? rt::mixed_sched() : std::vector<std::string>{};
   rt::KernelMeta m;
   std::string compiler, why;
   auto fail = [&why]() {

@@ -621,11 +621,17 @@ bool jit_kernels(const SceneImage &img, int variant, uint32_t max_visits, bool f
   return true;
 }
 
+// The mixed walk is built with the max-ilp scheduler since round 6: under LLVM 22 it ran final_scene 485.5 / 477.0 /
+// 486.5 ms against 488.2 / 500.3 / 497.8 with the default strategy (max-memory-clause level; round 5 under LLVM 20:
+// max-ilp level; profiles/r06_ab_mixed_sched.jsonl).  RT_MIXED_SCHED=<strategy> (A/B; 0: the default) builds it with another.
+std::vector<std::string> mixed_sched() { return sched_options("RT_MIXED_SCHED", true); }
+
 bool jit_mixed_kernels(const SceneImage &img, int variant, JitKernels *out, std::string *why) {
   out->visits = 0;
   out->folded = false;
-  if (!build_module(jit_mixed_source(img, variant), "rt_mixed", out, why)) return false;
-  raise_residency([&](int w) { return jit_mixed_source(img, variant, w); }, "rt_mixed", out);
+  const std::vector<std::string> sched = mixed_sched();
+  if (!build_module(jit_mixed_source(img, variant), "rt_mixed", out, why, sched)) return false;
+  raise_residency([&](int w) { return jit_mixed_source(img, variant, w); }, "rt_mixed", out, sched);
   return true;
 }
 

@@ -67,6 +67,7 @@ std::vector<std::string> jit_options(const std::string &arch, const std::vector<
 // RT_ACCEL_SCHED)
 std::vector<std::string> static_sched(const SceneImage &img);
 std::vector<std::string> accel_sched();
+std::vector<std::string> mixed_sched();
 // the verified walk's default waves request is kept only when its build has no more scratch than this (0)
 bool accel_waves_build_kept(int scratch_bytes);
 // compile `src` for `arch` with the run-time compiler and options (no device) and read <prefix>_render's figures
